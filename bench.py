@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpoints/s of k-th-NN distance (k=100) on 1B uniform float3.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--points P] [--k K] [--variant V]
+
+Launched by the driver as ``torch.distributed.run --nproc-per-node N bench.py --gpus N``
+for N > 1 (one rank per GPU, RCCL over xGMI). Each rank owns the reference's
+block partition [floor(P*r/N), floor(P*(r+1)/N)) of one global synthetic uniform-random
+point set held in pinned host memory. One timed step = the BASELINE.md clock: host
+points -> H2D -> (unordered variant) spatial redistribution + bucket-tree k-NN + halo
+exchange + result return -> distances back in host memory. W untimed warmup steps, then
+K steps bracketed by barrier + device sync; the max over ranks is reported.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm  # noqa: E402
+
+METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--points", type=float, default=1e9)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--variant", choices=["unordered", "prepartitioned"], default="unordered")
+    ap.add_argument("--phases", action="store_true", help="print per-phase times (adds syncs)")
+    ap.add_argument("--stats", action="store_true", help="collect k-NN kernel counters")
+    return ap.parse_args()
+
+
+def make_points(n_total: int, rank: int, size: int, device, variant: str) -> torch.Tensor:
+    """This rank's slice of the global synthetic set, in pinned host memory."""
+    b = n_total * rank // size
+    e = n_total * (rank + 1) // size
+    n = e - b
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    host = torch.empty((n, 3), dtype=torch.float32, pin_memory=True)
+    chunk = 1 << 26
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        d = torch.rand((m, 3), generator=g, device=device, dtype=torch.float32)
+        if variant == "prepartitioned":
+            # spatially tiled files: rank r owns the slab [r/size, (r+1)/size) in x
+            d[:, 0] = (d[:, 0] + rank) / size
+        host[s:s + m].copy_(d)
+    torch.cuda.synchronize(device)
+    return host
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+        comm = TorchComm(device)
+    else:
+        comm = SingleComm(device)
+    n_total = int(args.points)
+    cfg = KnnConfig(k=args.k, collect_stats=args.stats)
+
+    host_pts = make_points(n_total, rank, world, device, args.variant)
+    host_out = torch.empty(host_pts.shape[0], dtype=torch.float32, pin_memory=True)
+
+    info_last = None
+
+    def step():
+        nonlocal info_last
+        info = PL.RunInfo(PL.PhaseTimer(args.phases, device))
+        pts = host_pts.to(device, non_blocking=True)
+        if args.variant == "unordered":
+            out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total)
+        else:
+            out = PL.prepartitioned_knn(pts, comm, cfg, info)
+        host_out.copy_(out, non_blocking=True)
+        torch.cuda.synchronize(device)
+        info_last = info
+
+    for _ in range(args.warmup):
+        step()
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    comm.allreduce_(t, "max")
+    elapsed = float(t.item())
+
+    ms = elapsed / args.steps * 1e3
+    value = n_total * args.steps / elapsed / 1e6
+    # sanity: distances must be finite and positive for uniform data with k <= n
+    finite = bool(torch.isfinite(host_out).all()) if host_out.numel() else True
+    if rank == 0:
+        if args.phases or args.stats:
+            print(json.dumps({"phases_s": info_last.timer.times, "counts": info_last.counts,
+                              "knn_stats": info_last.stats.counters}), file=sys.stderr)
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mpoints/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "fp32",
+            "data": "synthetic uniform-random float3 in [0,1)^3 (pinned host memory), no file I/O",
+            "config": {
+                "model": f"{args.variant}Data k-th-NN distance, k={args.k}",
+                "global_batch": n_total,
+                "seq_len": None,
+                "parallelism": f"spatial-redistribute+halo x{world}" if args.variant == "unordered"
+                else f"halo x{world}",
+                "k": args.k,
+                "all_finite": finite,
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,108 @@
+"""In-tree build of the native libraries.
+
+* ``lib/liblsknn_host.so``  — C++17 host runtime (I/O, CLI, peer schedule, CPU oracle),
+  built with g++.
+* ``lib/liblsknn_hip.so``   — hand-written gfx950 HIP kernels, built with
+  ``hipcc --offload-arch=gfx950`` (cross-compiles without a GPU).
+
+Both are rebuilt only when a source or header is newer than the library. The
+libraries are git-ignored but travel to the GPU box with the working tree.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+HOST_LIB = os.path.join(LIB_DIR, "liblsknn_host.so")
+HIP_LIB = os.path.join(LIB_DIR, "liblsknn_hip.so")
+GPU_ARCH = os.environ.get("LSKNN_GPU_ARCH", "gfx950")
+
+# -ffp-contract=off everywhere: the canonical dist2 association must not be changed by
+# FMA contraction; correctly-rounded sqrtf requires no fast-math.
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math"]
+HOST_FLAGS = COMMON_FLAGS + ["-mfma", "-mavx2", "-pthread", "-Wall", "-Wno-unused-function"]
+HIP_FLAGS = COMMON_FLAGS + [f"--offload-arch={GPU_ARCH}", "-Wno-unused-result"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build the gfx950 kernels)")
+
+
+def _sources(sub: str, ext: str) -> list[str]:
+    return sorted(glob.glob(os.path.join(CSRC, sub, f"*.{ext}")))
+
+
+def _headers() -> list[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True))
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + proc.stdout)
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    srcs = _sources("host", "cpp")
+    if force or _stale(HOST_LIB, srcs + _headers()):
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = HOST_LIB + ".tmp"
+        cmd = ["g++", *HOST_FLAGS, "-shared", "-o", tmp, *srcs]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        _run(cmd)
+        os.replace(tmp, HOST_LIB)
+    return HOST_LIB
+
+
+def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
+    srcs = _sources("hip", "hip")
+    if not (force or _stale(HIP_LIB, srcs + _headers())):
+        return HIP_LIB
+    hipcc = _hipcc()
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    hdrs = _headers()
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            cmd = [hipcc, *HIP_FLAGS, "-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            _run(cmd)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = HIP_LIB + ".tmp"
+    _run([hipcc, f"--offload-arch={GPU_ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
+    os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_all(force: bool = False, verbose: bool = False) -> tuple[str, str]:
+    return build_host(force, verbose), build_hip(force, verbose)
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for p in build_all(force=force, verbose=True):
+        print(p)

@@ -1,0 +1,86 @@
+// Device-side helpers shared by the lsknn gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../common.h"
+#include "lsk_hip.h"
+
+namespace lsk {
+
+constexpr int kWave = 64;
+constexpr int kBucket = 64;  // points per tree leaf == queries per wave group
+
+// Constant-address-space view of read-only global data: uniform-address loads through
+// it become scalar (SMEM) loads, so wave-uniform candidate points arrive in SGPRs and
+// cost no VALU or LDS issue slots.
+typedef const __attribute__((address_space(4))) float *cfloat_p;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) v4f *cfloat4_p;
+typedef const __attribute__((address_space(4))) uint32_t *cuint_p;
+
+__device__ __forceinline__ cfloat_p as_const(const float *p) { return (cfloat_p)(p); }
+__device__ __forceinline__ cfloat4_p as_const4(const float *p) { return (cfloat4_p)(p); }
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5.5 T1): blocks are dealt
+// round-robin over the 8 XCDs; give each XCD a contiguous range of logical blocks so
+// spatially adjacent query groups share an L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
+  const uint32_t q = nblk / 8, r = nblk % 8;
+  const uint32_t xcd = bid % 8, local = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+}  // namespace lsk
+
+// -------------------------------------------------------------------- host-side errors
+namespace lsk {
+void set_last_error(const std::string &msg);
+}
+
+#define LSK_CHECK_LAUNCH(name)                                                        \
+  do {                                                                                \
+    hipError_t e__ = hipGetLastError();                                               \
+    if (e__ != hipSuccess) {                                                          \
+      lsk::set_last_error(std::string(name) + ": " + hipGetErrorString(e__));         \
+      return (int)e__;                                                                \
+    }                                                                                 \
+  } while (0)
+
+#define LSK_HIP(call)                                                                 \
+  do {                                                                                \
+    hipError_t e__ = (call);                                                          \
+    if (e__ != hipSuccess) {                                                          \
+      lsk::set_last_error(std::string(#call) + ": " + hipGetErrorString(e__));        \
+      return (int)e__;                                                                \
+    }                                                                                 \
+  } while (0)
+
+static inline unsigned lsk_blocks(int64_t n, int per_block, unsigned cap = 0) {
+  int64_t b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (cap && b > (int64_t)cap) b = cap;
+  return (unsigned)b;
+}

@@ -1,0 +1,120 @@
+// lsknn gfx950 kernel library — C ABI (ctypes from Python; the caller owns all memory).
+//
+// Every entry point takes the HIP stream to launch on (torch's current stream when
+// called from Python) and never allocates, synchronises or copies to the host, so a
+// whole local pipeline can be captured into a hipGraph. Workspace sizes come from the
+// *_ws_bytes queries. Return value: 0 on success, a hipError_t otherwise
+// (lsk_hip_last_error() has the message).
+//
+// Layout conventions
+//   points   : packed float3 (12 B) arrays; arrays read by the k-NN kernel must carry
+//              64 points of readable padding after the last point (scalar loads fetch
+//              candidates in 8-point chunks).
+//   tree     : implicit complete binary tree over 64-point Morton buckets. Node i
+//              (root = 1) is two float4: lo.xyz + lo.w = max squared k-NN radius of the
+//              queries below it (halo publishing), hi.xyz + hi.w unused. Leaves are at
+//              level `depth`: node (1<<depth)+b covers sorted points [64b, 64b+64).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int lsk_hip_abi_version(void);
+const char *lsk_hip_last_error(void);
+int lsk_hip_device_info(int device, char *buf, int buflen);
+
+// ---- bounds / Morton / permutation helpers ---------------------------------------
+size_t lsk_hip_bounds_ws_bytes(int64_t n);
+// box_out: 8 floats on device: lo.xyz, hi.xyz, cube scale (1024/extent), extent.
+int lsk_hip_bounds(const float *pts, int64_t n, float *box_out, void *ws, void *stream);
+// Recompute box_out[6..7] from box_out[0..5] (after a cross-rank min/max reduction).
+int lsk_hip_box_finalize(float *box, void *stream);
+// keys[i] = Morton30(pts[i]) in the cube of `box`; vals[i] = i.
+int lsk_hip_morton(const float *pts, int64_t n, const float *box, uint32_t *keys,
+                   uint32_t *vals, void *stream);
+// dst[i] = src[idx[i]] (float3 gather).
+int lsk_hip_gather3(const float *src, const uint32_t *idx, int64_t n, float *dst, void *stream);
+// dst[idx[i]] = src[i] (float scatter), optional sqrt-finalisation.
+int lsk_hip_scatter1(const float *src, const uint32_t *idx, int64_t n, float *dst,
+                     int finalize_sqrt, void *stream);
+// out[i] = finalize(src[i]) (sqrt unless inf).
+int lsk_hip_finalize(const float *src, int64_t n, float *dst, void *stream);
+// keys[i] = destination rank of point i: number of splitters s with (morton>>shift) >= s.
+int lsk_hip_dest_rank(const uint32_t *morton, int64_t n, const uint32_t *splitters,
+                      int nsplit, int shift, uint32_t *dest, uint32_t *vals, void *stream);
+// hist[morton >> shift] += 1 (hist: uint32 of size 1<<(30-shift), zeroed by caller).
+int lsk_hip_key_histogram(const uint32_t *keys, int64_t n, int shift, uint32_t *hist,
+                          void *stream);
+// counts[dest[i]] += 1 for dest < ndest (counts zeroed by caller).
+int lsk_hip_count_dest(const uint32_t *dest, int64_t n, int ndest, uint32_t *counts,
+                       void *stream);
+
+// ---- LSD radix sort of (uint32 key, uint32 value) pairs ------------------------------
+size_t lsk_hip_sort_ws_bytes(int64_t n);
+// Sorts by key bits [0, key_bits). Uses keys_alt/vals_alt as ping-pong buffers;
+// *result_in_alt is set to 1 if the sorted output ended in the alt buffers.
+int lsk_hip_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                       int64_t n, int key_bits, void *ws, int *result_in_alt, void *stream);
+
+// ---- bucket tree ---------------------------------------------------------------------
+int lsk_hip_tree_depth(int64_t n);          // depth for 64-point buckets
+int64_t lsk_hip_tree_nodes(int64_t n);      // number of node slots (2^(depth+1))
+int lsk_hip_build_tree(const float *sorted_pts, int64_t n, float *nodes, void *stream);
+// leaves' lo.w = max over the bucket's queries of d2[i]; propagated to all levels.
+int lsk_hip_tree_set_radii(float *nodes, int64_t n, const float *d2_sorted, void *stream);
+
+// ---- k-th-distance selection ----------------------------------------------------------
+typedef struct lsk_tree_view {
+  const float *pts;    // sorted points (padded)
+  const float *nodes;  // node array
+  int64_t n;
+  int32_t depth;
+  int32_t pad;
+} lsk_tree_view;
+
+typedef struct lsk_knn_args {
+  const float *qpts;        // sorted query points; groups of 64 consecutive queries
+  int64_t nq;
+  const uint32_t *groups;   // optional list of query groups to (re)process
+  int64_t ngroups;          // length of `groups` (ignored when groups == NULL)
+  lsk_tree_view tree[2];
+  int32_t ntrees;
+  int32_t k;
+  float cut2;               // (-r R)^2 as float; +inf by default
+  float r_hint2;            // global estimate of the k-th squared distance
+  float *out_d2;            // [nq] k-th squared distance per query (sorted order)
+  unsigned long long *stats;  // optional [16] 64-bit counters (NULL = off)
+  uint32_t *qstatus;        // optional [nq] per-query status bits (NULL = off)
+} lsk_knn_args;
+
+int lsk_hip_knn(const lsk_knn_args *args, void *stream);
+
+// ---- halo exchange -------------------------------------------------------------------
+// Published tree: the top `levels` levels of a tree (node slots 1 .. 2^levels-1... up to
+// 2^(levels+1)), each node 8 floats (lo.xyz, r2, hi.xyz, pad).
+// mask[i] bit j set iff point i must be sent to rank j (j != self).
+int lsk_hip_halo_mask(const float *pts, int64_t n, const float *pub, const int64_t *pub_off,
+                      const int32_t *pub_depth, int nranks, int self, uint64_t *mask,
+                      void *stream);
+// Flag query groups (64 consecutive sorted queries) that may have a closer halo point:
+// flags[g] = 1 iff some halo leaf box is strictly closer to one of the group's queries
+// than that query's current k-th squared distance qd2.
+int lsk_hip_flag_query_groups(const float *qpts, const float *qd2, int64_t nq,
+                              const float *halo_nodes, int32_t halo_depth, int64_t nhalo,
+                              uint32_t *flags, void *stream);
+// Compacts indices i with flags[i] != 0 into list; *count (device) receives the count.
+int lsk_hip_compact_flags(const uint32_t *flags, int64_t n, uint32_t *list, uint32_t *count,
+                          void *stream);
+// For each destination rank j: writes the points with mask bit j into send buffer at
+// offsets[j] + (running cursor). cursors: device [nranks] zeroed by caller.
+int lsk_hip_halo_pack(const float *pts, const uint64_t *mask, int64_t n, int nranks,
+                      const int64_t *offsets, uint32_t *cursors, float *send, void *stream);
+int lsk_hip_mask_counts(const uint64_t *mask, int64_t n, int nranks, uint32_t *counts,
+                        void *stream);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,203 @@
+// Hand-written LSD radix sort of (uint32 key, uint32 value) pairs for gfx950.
+//
+// Used for the Morton sort that precedes the bucket k-d tree build (the reference's
+// cukd::buildTree sorts with thrust, unorderedDataVariant.cu:161 [inferred]; SURVEY
+// §7.5 H5) and for the destination-rank partition of the spatial redistribution.
+//
+// Per 8-bit digit pass (reduce-then-scan, stable):
+//   upsweep   : each block histograms its contiguous chunk          -> counts[d][blk]
+//   scan      : one 1024-thread block scans counts (digit-major)     -> global offsets
+//   downsweep : each block walks its chunk in 4096-element tiles; a wave ranks its 64
+//               lanes per row with 8 ballots (wave-64 multisplit), waves are combined
+//               through LDS prefix sums, the tile is staged in LDS in digit order and
+//               written out in coalesced digit runs.
+#include "dev.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / lsk::kWave;
+constexpr int kRadix = 256;
+constexpr int kRows = 16;                              // rows of 64 per wave per tile
+constexpr int kTile = kWaves * lsk::kWave * kRows;     // 4096 elements
+constexpr unsigned kMaxBlocks = 2048;
+
+__device__ __forceinline__ int64_t chunk_begin(int64_t n, unsigned b, unsigned nb) {
+  return (int64_t)(((__uint128_t)n * b) / nb);
+}
+
+__global__ __launch_bounds__(kThreads) void upsweep_kernel(const uint32_t *__restrict__ keys,
+                                                           int64_t n, int shift,
+                                                           uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[kWaves][kRadix];
+  const int t = threadIdx.x, w = t >> 6;
+  for (int i = t; i < kWaves * kRadix; i += kThreads) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t cb = chunk_begin(n, blockIdx.x, gridDim.x);
+  const int64_t ce = chunk_begin(n, blockIdx.x + 1, gridDim.x);
+  for (int64_t i = cb + t; i < ce; i += kThreads) atomicAdd(&h[w][(keys[i] >> shift) & 255u], 1u);
+  __syncthreads();
+  uint32_t s = 0;
+  for (int j = 0; j < kWaves; j++) s += h[j][t];
+  counts[(size_t)t * gridDim.x + blockIdx.x] = s;
+}
+
+// Block-wide exclusive scan of one value per thread (kThreads threads).
+template <int NT>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *wave_tot,
+                                                         uint32_t *total) {
+  const int lane = lsk::lane_id(), w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wave_tot[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+  for (int j = 0; j < NT / 64; j++) {
+    uint32_t c = wave_tot[j];
+    if (j < w) pre += c;
+    tot += c;
+  }
+  if (total) *total = tot;
+  __syncthreads();
+  return pre + x - v;
+}
+
+__global__ __launch_bounds__(1024) void scan_kernel(uint32_t *__restrict__ counts, int64_t total) {
+  __shared__ uint32_t wave_tot[16];
+  const int t = threadIdx.x;
+  const int64_t seg = (total + 1023) / 1024;
+  const int64_t b = t * seg, e = b + seg < total ? b + seg : total;
+  uint32_t s = 0;
+  for (int64_t i = b; i < e; i++) s += counts[i];
+  uint32_t run = block_exclusive_scan<1024>(s, wave_tot, nullptr);
+  for (int64_t i = b; i < e; i++) {
+    uint32_t c = counts[i];
+    counts[i] = run;
+    run += c;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void downsweep_kernel(
+    const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+    uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int64_t n, int shift,
+    const uint32_t *__restrict__ offsets) {
+  __shared__ uint32_t wave_cnt[kWaves][kRadix];
+  __shared__ uint32_t run_base[kRadix];
+  __shared__ uint32_t tile_start[kRadix];
+  __shared__ uint32_t tile_total[kRadix];
+  __shared__ uint32_t wave_tot[kWaves];
+  __shared__ uint32_t stage_k[kTile];
+  __shared__ uint32_t stage_v[kTile];
+
+  const int t = threadIdx.x, w = t >> 6, lane = lsk::lane_id();
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const int64_t cb = chunk_begin(n, blockIdx.x, gridDim.x);
+  const int64_t ce = chunk_begin(n, blockIdx.x + 1, gridDim.x);
+  run_base[t] = offsets[(size_t)t * gridDim.x + blockIdx.x];
+
+  for (int64_t tb = cb; tb < ce; tb += kTile) {
+    const int tn = (int)((ce - tb) < kTile ? (ce - tb) : kTile);
+    for (int i = t; i < kWaves * kRadix; i += kThreads) (&wave_cnt[0][0])[i] = 0;
+    __syncthreads();
+
+    uint32_t kr[kRows], vr[kRows], offr[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+      const int e = w * (lsk::kWave * kRows) + r * lsk::kWave + lane;
+      const bool valid = e < tn;
+      kr[r] = valid ? kin[tb + e] : 0u;
+      vr[r] = valid ? vin[tb + e] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+      const int e = w * (lsk::kWave * kRows) + r * lsk::kWave + lane;
+      const bool valid = e < tn;
+      const uint32_t d = (kr[r] >> shift) & 255u;
+      uint64_t match = __ballot(valid);
+#pragma unroll
+      for (int bit = 0; bit < 8; bit++) {
+        const bool on = (d >> bit) & 1u;
+        const uint64_t b = __ballot(on);
+        match &= on ? b : ~b;
+      }
+      const uint32_t before = valid ? wave_cnt[w][d] : 0u;
+      offr[r] = before + (uint32_t)__popcll(match & lt_mask);
+      // the highest lane of each digit group publishes the new running count
+      if (valid && (match >> lane) == 1ull) wave_cnt[w][d] = before + (uint32_t)__popcll(match);
+    }
+    __syncthreads();
+    {
+      uint32_t s = 0;
+#pragma unroll
+      for (int j = 0; j < kWaves; j++) {
+        uint32_t c = wave_cnt[j][t];
+        wave_cnt[j][t] = s;
+        s += c;
+      }
+      tile_total[t] = s;
+      tile_start[t] = block_exclusive_scan<kThreads>(s, wave_tot, nullptr);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+      const int e = w * (lsk::kWave * kRows) + r * lsk::kWave + lane;
+      if (e < tn) {
+        const uint32_t d = (kr[r] >> shift) & 255u;
+        const uint32_t lp = tile_start[d] + wave_cnt[w][d] + offr[r];
+        stage_k[lp] = kr[r];
+        stage_v[lp] = vr[r];
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < tn; i += kThreads) {
+      const uint32_t k = stage_k[i];
+      const uint32_t d = (k >> shift) & 255u;
+      const uint32_t g = run_base[d] + (uint32_t)i - tile_start[d];
+      kout[g] = k;
+      vout[g] = stage_v[i];
+    }
+    __syncthreads();
+    run_base[t] += tile_total[t];
+    __syncthreads();
+  }
+}
+
+unsigned sort_blocks(int64_t n) { return lsk_blocks(n, kTile, kMaxBlocks); }
+
+}  // namespace
+
+extern "C" size_t lsk_hip_sort_ws_bytes(int64_t n) {
+  return (size_t)kRadix * sort_blocks(n) * sizeof(uint32_t) + 256;
+}
+
+extern "C" int lsk_hip_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt,
+                                  uint32_t *vals_alt, int64_t n, int key_bits, void *ws,
+                                  int *result_in_alt, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  *result_in_alt = 0;
+  if (n <= 1 || key_bits <= 0) return 0;
+  if (n >= (int64_t(1) << 32)) {
+    lsk::set_last_error("sort_pairs: n must be < 2^32");
+    return 1;
+  }
+  const unsigned nb = sort_blocks(n);
+  uint32_t *counts = (uint32_t *)ws;
+  uint32_t *ki = keys, *vi = vals, *ko = keys_alt, *vo = vals_alt;
+  int passes = 0;
+  for (int shift = 0; shift < key_bits; shift += 8, passes++) {
+    upsweep_kernel<<<nb, kThreads, 0, s>>>(ki, n, shift, counts);
+    LSK_CHECK_LAUNCH("sort_upsweep");
+    scan_kernel<<<1, 1024, 0, s>>>(counts, (int64_t)kRadix * nb);
+    LSK_CHECK_LAUNCH("sort_scan");
+    downsweep_kernel<<<nb, kThreads, 0, s>>>(ki, vi, ko, vo, n, shift, counts);
+    LSK_CHECK_LAUNCH("sort_downsweep");
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  *result_in_alt = passes & 1;
+  return 0;
+}

@@ -1,0 +1,105 @@
+// Bucket k-d tree over Morton-sorted points (gfx950).
+//
+// The reference builds a left-balanced object-median k-d tree in place with
+// cukd::buildTree (unorderedDataVariant.cu:161, prePartitionedDataVariant.cu:271,
+// [inferred]). Here the tree comes from the Morton sort: sorted points are cut into
+// 64-point buckets (one wavefront of candidates per leaf), and an implicit complete
+// binary tree over the buckets stores one AABB per node. Consecutive Morton buckets
+// are spatially coherent, so each node's box is tight; splits follow the Morton
+// (spatial-median, round-robin axis) order of the keys.
+#include "dev.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void leaf_kernel(const float *__restrict__ pts, int64_t n,
+                                                   float *__restrict__ nodes, int depth,
+                                                   int64_t nleaf_slots) {
+  const int64_t leaf = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (leaf >= nleaf_slots) return;
+  const int lane = lsk::lane_id();
+  const int64_t i = leaf * lsk::kBucket + lane;
+  const float inf = __builtin_inff();
+  float lx = inf, ly = inf, lz = inf, hx = -inf, hy = -inf, hz = -inf;
+  if (i < n) {
+    lx = hx = pts[3 * i];
+    ly = hy = pts[3 * i + 1];
+    lz = hz = pts[3 * i + 2];
+  }
+  lx = lsk::wave_min(lx); ly = lsk::wave_min(ly); lz = lsk::wave_min(lz);
+  hx = lsk::wave_max(hx); hy = lsk::wave_max(hy); hz = lsk::wave_max(hz);
+  if (lane == 0) {
+    float4 *nd = (float4 *)nodes + 2 * (((int64_t)1 << depth) + leaf);
+    nd[0] = make_float4(lx, ly, lz, 0.f);
+    nd[1] = make_float4(hx, hy, hz, 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void levelup_kernel(float *__restrict__ nodes, int level,
+                                                      int radii_only) {
+  const int64_t cnt = (int64_t)1 << level;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cnt) return;
+  const int64_t node = cnt + j;
+  float4 *nd = (float4 *)nodes;
+  const float4 al = nd[2 * (2 * node)], ah = nd[2 * (2 * node) + 1];
+  const float4 bl = nd[2 * (2 * node + 1)], bh = nd[2 * (2 * node + 1) + 1];
+  if (radii_only) {
+    nd[2 * node].w = fmaxf(al.w, bl.w);
+  } else {
+    nd[2 * node] = make_float4(fminf(al.x, bl.x), fminf(al.y, bl.y), fminf(al.z, bl.z),
+                               fmaxf(al.w, bl.w));
+    nd[2 * node + 1] = make_float4(fmaxf(ah.x, bh.x), fmaxf(ah.y, bh.y), fmaxf(ah.z, bh.z), 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void leaf_radius_kernel(const float *__restrict__ d2,
+                                                          int64_t n, float *__restrict__ nodes,
+                                                          int depth, int64_t nleaf_slots) {
+  const int64_t leaf = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (leaf >= nleaf_slots) return;
+  const int64_t i = leaf * lsk::kBucket + lsk::lane_id();
+  float r = i < n ? d2[i] : 0.f;
+  r = lsk::wave_max(r);
+  if (lsk::lane_id() == 0) nodes[8 * (((int64_t)1 << depth) + leaf) + 3] = r;
+}
+
+}  // namespace
+
+extern "C" int lsk_hip_tree_depth(int64_t n) {
+  int64_t nb = (n + lsk::kBucket - 1) / lsk::kBucket;
+  int d = 0;
+  while (((int64_t)1 << d) < nb) d++;
+  return d;
+}
+
+extern "C" int64_t lsk_hip_tree_nodes(int64_t n) {
+  return (int64_t)2 << lsk_hip_tree_depth(n);
+}
+
+extern "C" int lsk_hip_build_tree(const float *sorted_pts, int64_t n, float *nodes,
+                                  void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int depth = lsk_hip_tree_depth(n);
+  const int64_t slots = (int64_t)1 << depth;
+  leaf_kernel<<<lsk_blocks(slots, 4), 256, 0, s>>>(sorted_pts, n, nodes, depth, slots);
+  LSK_CHECK_LAUNCH("tree_leaf");
+  for (int l = depth - 1; l >= 0; l--) {
+    levelup_kernel<<<lsk_blocks((int64_t)1 << l, 256), 256, 0, s>>>(nodes, l, 0);
+    LSK_CHECK_LAUNCH("tree_levelup");
+  }
+  return 0;
+}
+
+extern "C" int lsk_hip_tree_set_radii(float *nodes, int64_t n, const float *d2_sorted,
+                                      void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int depth = lsk_hip_tree_depth(n);
+  const int64_t slots = (int64_t)1 << depth;
+  leaf_radius_kernel<<<lsk_blocks(slots, 4), 256, 0, s>>>(d2_sorted, n, nodes, depth, slots);
+  LSK_CHECK_LAUNCH("tree_leaf_radius");
+  for (int l = depth - 1; l >= 0; l--) {
+    levelup_kernel<<<lsk_blocks((int64_t)1 << l, 256), 256, 0, s>>>(nodes, l, 1);
+    LSK_CHECK_LAUNCH("tree_levelup_radius");
+  }
+  return 0;
+}

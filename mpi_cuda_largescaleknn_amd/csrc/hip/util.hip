@@ -1,0 +1,271 @@
+// Bounds, Morton keys, gathers/scatters and small partitioning helpers (gfx950).
+//
+// Replaces the reference's host-side O(N) bounds loop (prePartitionedDataVariant.cu:
+// 230-232) with a device reduction, and provides the Morton/partition primitives the
+// spatial redistribution (unordered variant) is built from.
+#include "dev.h"
+
+#include <cstdio>
+#include <mutex>
+
+namespace lsk {
+static std::mutex g_err_mu;
+static std::string g_err;
+void set_last_error(const std::string &msg) {
+  std::lock_guard<std::mutex> g(g_err_mu);
+  g_err = msg;
+}
+}  // namespace lsk
+
+extern "C" int lsk_hip_abi_version(void) { return 1; }
+
+extern "C" const char *lsk_hip_last_error(void) {
+  static thread_local std::string copy;
+  std::lock_guard<std::mutex> g(lsk::g_err_mu);
+  copy = lsk::g_err;
+  return copy.c_str();
+}
+
+extern "C" int lsk_hip_device_info(int device, char *buf, int buflen) {
+  hipDeviceProp_t p;
+  LSK_HIP(hipGetDeviceProperties(&p, device));
+  std::snprintf(buf, (size_t)buflen, "%s arch=%s CUs=%d lds/block=%zu mem=%zu", p.name,
+                p.gcnArchName, p.multiProcessorCount, (size_t)p.sharedMemPerBlock,
+                (size_t)p.totalGlobalMem);
+  return 0;
+}
+
+namespace {
+
+constexpr int kBoundsThreads = 256;
+constexpr unsigned kBoundsMaxBlocks = 2048;
+
+__global__ __launch_bounds__(kBoundsThreads) void bounds_partial_kernel(
+    const float *__restrict__ pts, int64_t n, float *__restrict__ partial) {
+  const float inf = __builtin_inff();
+  float l0 = inf, l1 = inf, l2 = inf, h0 = -inf, h1 = -inf, h2 = -inf;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+    l0 = fminf(l0, x); l1 = fminf(l1, y); l2 = fminf(l2, z);
+    h0 = fmaxf(h0, x); h1 = fmaxf(h1, y); h2 = fmaxf(h2, z);
+  }
+  l0 = lsk::wave_min(l0); l1 = lsk::wave_min(l1); l2 = lsk::wave_min(l2);
+  h0 = lsk::wave_max(h0); h1 = lsk::wave_max(h1); h2 = lsk::wave_max(h2);
+  __shared__ float red[kBoundsThreads / lsk::kWave][6];
+  const int w = threadIdx.x >> 6;
+  if (lsk::lane_id() == 0) {
+    red[w][0] = l0; red[w][1] = l1; red[w][2] = l2;
+    red[w][3] = h0; red[w][4] = h1; red[w][5] = h2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float v = red[0][threadIdx.x];
+    for (int j = 1; j < kBoundsThreads / lsk::kWave; j++)
+      v = threadIdx.x < 3 ? fminf(v, red[j][threadIdx.x]) : fmaxf(v, red[j][threadIdx.x]);
+    partial[6 * blockIdx.x + threadIdx.x] = v;
+  }
+}
+
+__device__ void finalize_box(float *box) {
+  const float ex = fmaxf(fmaxf(box[3] - box[0], box[4] - box[1]), box[5] - box[2]);
+  const bool ok = ex > 0.f && ex < __builtin_inff();
+  box[6] = ok ? 1024.f / ex : 0.f;
+  box[7] = ok ? ex : 0.f;
+}
+
+__global__ void bounds_final_kernel(const float *__restrict__ partial, int nb,
+                                    float *__restrict__ box) {
+  const int t = threadIdx.x;  // 64 threads
+  const float inf = __builtin_inff();
+  float v[6] = {inf, inf, inf, -inf, -inf, -inf};
+  for (int b = t; b < nb; b += 64) {
+    for (int a = 0; a < 3; a++) v[a] = fminf(v[a], partial[6 * b + a]);
+    for (int a = 3; a < 6; a++) v[a] = fmaxf(v[a], partial[6 * b + a]);
+  }
+  for (int a = 0; a < 3; a++) v[a] = lsk::wave_min(v[a]);
+  for (int a = 3; a < 6; a++) v[a] = lsk::wave_max(v[a]);
+  if (t == 0) {
+    for (int a = 0; a < 6; a++) box[a] = v[a];
+    finalize_box(box);
+  }
+}
+
+__global__ void box_finalize_kernel(float *box) {
+  if (threadIdx.x == 0) finalize_box(box);
+}
+
+__global__ __launch_bounds__(256) void morton_kernel(const float *__restrict__ pts, int64_t n,
+                                                     const float *__restrict__ box,
+                                                     uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+  const float ox = box[0], oy = box[1], oz = box[2], s = box[6];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t ix = lsk::morton_quant(pts[3 * i], ox, s);
+    const uint32_t iy = lsk::morton_quant(pts[3 * i + 1], oy, s);
+    const uint32_t iz = lsk::morton_quant(pts[3 * i + 2], oz, s);
+    keys[i] = lsk::morton3(ix, iy, iz);
+    if (vals) vals[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void gather3_kernel(const float *__restrict__ src,
+                                                      const uint32_t *__restrict__ idx,
+                                                      int64_t n, float *__restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t j = idx[i];
+    const float x = src[3 * j], y = src[3 * j + 1], z = src[3 * j + 2];
+    dst[3 * i] = x; dst[3 * i + 1] = y; dst[3 * i + 2] = z;
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter1_kernel(const float *__restrict__ src,
+                                                       const uint32_t *__restrict__ idx,
+                                                       int64_t n, float *__restrict__ dst,
+                                                       int fin) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = src[i];
+    dst[idx[i]] = fin ? lsk::final_distance(v) : v;
+  }
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__ src,
+                                                       int64_t n, float *__restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = lsk::final_distance(src[i]);
+}
+
+__global__ __launch_bounds__(256) void dest_rank_kernel(const uint32_t *__restrict__ morton,
+                                                        int64_t n,
+                                                        const uint32_t *__restrict__ split,
+                                                        int nsplit, int shift,
+                                                        uint32_t *__restrict__ dest,
+                                                        uint32_t *__restrict__ vals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t key = morton[i] >> shift;
+    // number of splitters <= key (splitters are ascending bin starts of ranks 1..P-1)
+    int lo = 0, hi = nsplit;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (split[mid] <= key) lo = mid + 1; else hi = mid;
+    }
+    dest[i] = (uint32_t)lo;
+    if (vals) vals[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void key_hist_kernel(const uint32_t *__restrict__ keys,
+                                                       int64_t n, int shift,
+                                                       uint32_t *__restrict__ hist) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    atomicAdd(&hist[keys[i] >> shift], 1u);
+}
+
+__global__ __launch_bounds__(256) void count_dest_kernel(const uint32_t *__restrict__ dest,
+                                                         int64_t n, int ndest,
+                                                         uint32_t *__restrict__ counts) {
+  __shared__ uint32_t loc[1024];
+  for (int i = threadIdx.x; i < ndest; i += blockDim.x) loc[i] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t d = dest[i];
+    if (d < (uint32_t)ndest) atomicAdd(&loc[d], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ndest; i += blockDim.x)
+    if (loc[i]) atomicAdd(&counts[i], loc[i]);
+}
+
+}  // namespace
+
+extern "C" size_t lsk_hip_bounds_ws_bytes(int64_t) { return kBoundsMaxBlocks * 6 * sizeof(float); }
+
+extern "C" int lsk_hip_bounds(const float *pts, int64_t n, float *box_out, void *ws,
+                              void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  unsigned nb = lsk_blocks(n, kBoundsThreads * 8, kBoundsMaxBlocks);
+  bounds_partial_kernel<<<nb, kBoundsThreads, 0, s>>>(pts, n, (float *)ws);
+  LSK_CHECK_LAUNCH("bounds_partial");
+  bounds_final_kernel<<<1, 64, 0, s>>>((const float *)ws, (int)nb, box_out);
+  LSK_CHECK_LAUNCH("bounds_final");
+  return 0;
+}
+
+extern "C" int lsk_hip_box_finalize(float *box, void *stream) {
+  box_finalize_kernel<<<1, 64, 0, (hipStream_t)stream>>>(box);
+  LSK_CHECK_LAUNCH("box_finalize");
+  return 0;
+}
+
+extern "C" int lsk_hip_morton(const float *pts, int64_t n, const float *box, uint32_t *keys,
+                              uint32_t *vals, void *stream) {
+  if (n <= 0) return 0;
+  morton_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(pts, n, box,
+                                                                             keys, vals);
+  LSK_CHECK_LAUNCH("morton");
+  return 0;
+}
+
+extern "C" int lsk_hip_gather3(const float *src, const uint32_t *idx, int64_t n, float *dst,
+                               void *stream) {
+  if (n <= 0) return 0;
+  gather3_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(src, idx, n,
+                                                                              dst);
+  LSK_CHECK_LAUNCH("gather3");
+  return 0;
+}
+
+extern "C" int lsk_hip_scatter1(const float *src, const uint32_t *idx, int64_t n, float *dst,
+                                int finalize_sqrt, void *stream) {
+  if (n <= 0) return 0;
+  scatter1_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(
+      src, idx, n, dst, finalize_sqrt);
+  LSK_CHECK_LAUNCH("scatter1");
+  return 0;
+}
+
+extern "C" int lsk_hip_finalize(const float *src, int64_t n, float *dst, void *stream) {
+  if (n <= 0) return 0;
+  finalize_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(src, n, dst);
+  LSK_CHECK_LAUNCH("finalize");
+  return 0;
+}
+
+extern "C" int lsk_hip_dest_rank(const uint32_t *morton, int64_t n, const uint32_t *splitters,
+                                 int nsplit, int shift, uint32_t *dest, uint32_t *vals,
+                                 void *stream) {
+  if (n <= 0) return 0;
+  dest_rank_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(
+      morton, n, splitters, nsplit, shift, dest, vals);
+  LSK_CHECK_LAUNCH("dest_rank");
+  return 0;
+}
+
+extern "C" int lsk_hip_key_histogram(const uint32_t *keys, int64_t n, int shift, uint32_t *hist,
+                                     void *stream) {
+  if (n <= 0) return 0;
+  key_hist_kernel<<<lsk_blocks(n, 256 * 8, 4096), 256, 0, (hipStream_t)stream>>>(keys, n, shift,
+                                                                               hist);
+  LSK_CHECK_LAUNCH("key_histogram");
+  return 0;
+}
+
+extern "C" int lsk_hip_count_dest(const uint32_t *dest, int64_t n, int ndest, uint32_t *counts,
+                                  void *stream) {
+  if (n <= 0) return 0;
+  if (ndest > 1024) {
+    lsk::set_last_error("count_dest: ndest > 1024");
+    return 1;
+  }
+  count_dest_kernel<<<lsk_blocks(n, 256 * 16, 2048), 256, 0, (hipStream_t)stream>>>(dest, n, ndest,
+                                                                                  counts);
+  LSK_CHECK_LAUNCH("count_dest");
+  return 0;
+}

@@ -1,0 +1,140 @@
+"""Single-rank k-th-nearest-neighbour distance engine.
+
+The "model" of this framework is the reference's per-rank work (SURVEY §1, L2+L4):
+build a k-d tree over the rank's points (cukd::buildTree, unorderedDataVariant.cu:161)
+and answer one k-NN query per point (runQuery/extractFinalResult, :75-103). Pipeline
+on the GPU — every step a hand-written gfx950 kernel on torch's current stream:
+
+    bounds -> Morton keys -> LSD radix sort -> gather -> bucket tree -> radix-select k-NN
+
+``LocalIndex`` is the reusable product of the first five steps (also used for the
+halo tree in the distributed pipelines).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+
+
+def cut2_of(max_radius: float) -> float:
+    """The reference stores maxRadius as float and compares squared distances against
+    cutOff*cutOff evaluated in float (FlexHeapCandidateList init, U:84-85)."""
+    r = np.float32(max_radius)
+    with np.errstate(over="ignore"):
+        return float(r * r)
+
+
+@dataclass
+class KnnConfig:
+    k: int
+    max_radius: float = math.inf
+    publish_levels: int = 12       # top tree levels published for halo filtering
+    collect_stats: bool = False
+
+    @property
+    def cut2(self) -> float:
+        return cut2_of(self.max_radius)
+
+
+@dataclass
+class LocalIndex:
+    n: int
+    pts: torch.Tensor        # [n + PAD, 3] Morton-sorted points (padded)
+    perm: torch.Tensor       # int32 [n]: sorted position -> row of the input array
+    nodes: torch.Tensor      # [2^(depth+1), 8] bucket-tree node boxes (lo.w = radius²)
+    depth: int
+    box: torch.Tensor        # [8] cube used for the Morton keys
+
+    @property
+    def device(self) -> torch.device:
+        return self.pts.device
+
+    def tree(self) -> tuple:
+        return (self.pts, self.nodes, self.n, self.depth)
+
+
+@dataclass
+class KnnStats:
+    counters: dict = field(default_factory=dict)
+
+    def add(self, raw: torch.Tensor) -> None:
+        names = ["evals", "leaves", "nodes", "hist_passes", "overflow_lanes", "underflow_lanes",
+                 "refine_lanes", "mismatch_lanes", "pass_limit_waves", "list_invalid_waves", "waves",
+                 "hint_lanes", "recorded_leaves"]
+        vals = raw.cpu().tolist()
+        for i, nm in enumerate(names):
+            self.counters[nm] = self.counters.get(nm, 0) + int(vals[i])
+
+
+def build_index(points: torch.Tensor, box: torch.Tensor | None = None) -> LocalIndex:
+    """Sort points along the Morton curve of `box` (default: their own bounds) and
+    build the bucket tree."""
+    points = points.contiguous()
+    n = points.shape[0]
+    if box is None:
+        box = K.bounds(points)
+    keys, iota = K.morton(points, box)
+    _, perm = K.sort_pairs(keys, iota, 30)
+    pts = K.gather3(points, perm, pad=K.PAD_POINTS)
+    nodes, depth = K.build_tree(pts, n)
+    return LocalIndex(n, pts, perm, nodes, depth, box)
+
+
+def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:
+    """Uniform-density estimate of the k-th squared distance (only used for groups
+    whose own extent is zero)."""
+    b = box.detach().cpu().tolist()
+    ext = [max(b[3 + a] - b[a], 0.0) for a in range(3)]
+    if not all(math.isfinite(e) for e in ext) or n_total <= 0:
+        return 1.0
+    nz = [e for e in ext if e > 0]
+    if not nz:
+        return 1.0
+    measure = math.prod(nz)
+    dim = len(nz)
+    rho = n_total / measure
+    unit = {1: 2.0, 2: math.pi, 3: 4.0 * math.pi / 3.0}[dim]
+    r = (k / (unit * rho)) ** (1.0 / dim)
+    return float(r * r)
+
+
+def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalIndex | None = None,
+          groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
+          stats: KnnStats | None = None, qstatus: torch.Tensor | None = None) -> torch.Tensor:
+    """k-th squared distance of every (or every listed group of) sorted query of
+    `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order."""
+    n = index.n
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=index.device)
+    if n == 0:
+        return out
+    if K.is_gpu(index.pts):
+        trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
+        raw = torch.zeros(16, dtype=torch.int64, device=index.device) if stats is not None else None
+        K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
+                  stats=raw, qstatus=qstatus)
+        if stats is not None:
+            stats.add(raw)
+        return out
+    pts = index.pts[:n]
+    if extra is not None and extra.n > 0:
+        pts = torch.cat([pts, extra.pts[:extra.n]])
+    out.copy_(K.kth_cpu(pts, index.pts[:n], cfg.k, cfg.cut2))
+    return out
+
+
+def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,
+                  stats: KnnStats | None = None) -> torch.Tensor:
+    """Distance from every point to its k-th nearest neighbour among `points`
+    (itself counted), in input order — the single-rank reference output."""
+    cfg = KnnConfig(k=k, max_radius=max_radius)
+    index = build_index(points)
+    hint2 = radius_hint2(index.box, index.n, k)
+    d2 = query(index, cfg, hint2, stats=stats)
+    out = torch.empty(index.n, dtype=torch.float32, device=points.device)
+    return K.scatter1(d2, index.perm, out, finalize=True)

@@ -1,0 +1,255 @@
+"""Tensor-level wrappers around the gfx950 kernels (and their CPU counterparts).
+
+Every function takes/returns torch tensors. CUDA (ROCm) tensors run the hand-written
+HIP kernels of ``csrc/hip`` on torch's current stream; CPU tensors run the C++ host
+runtime (``csrc/host``) or plain torch — that path exists for the CPU oracle, the
+``--device cpu`` mode and multi-process ``gloo`` tests. A CUDA tensor never falls back
+to the CPU path: if the kernel library is missing the call raises.
+
+uint32 data (Morton keys, indices) is stored in ``torch.int32`` tensors (same bits).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+
+import torch
+
+from .. import _native
+from .._native import KnnArgs, TreeView, check
+
+BUCKET = 64
+PAD_POINTS = 64  # readable padding required after point arrays read by the knn kernel
+
+
+def _nthreads() -> int:
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def is_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+# --------------------------------------------------------------------------- bounds
+def bounds(pts: torch.Tensor) -> torch.Tensor:
+    """AABB + Morton cube of an [n,3] float32 tensor -> [8] (lo.xyz, hi.xyz, scale, extent)."""
+    n = pts.shape[0]
+    if is_gpu(pts):
+        lib = _native.hip()
+        box = torch.empty(8, dtype=torch.float32, device=pts.device)
+        ws = torch.empty(lib.lsk_hip_bounds_ws_bytes(n) // 4 + 1, dtype=torch.float32, device=pts.device)
+        check(lib.lsk_hip_bounds(_ptr(pts), n, _ptr(box), _ptr(ws), _stream(pts)), "bounds")
+        return box
+    box = torch.empty(8, dtype=torch.float32)
+    _native.host().lsk_cpu_bounds(_ptr(pts.contiguous()), n, _ptr(box), _nthreads())
+    return box_finalize(box)
+
+
+def box_finalize(box: torch.Tensor) -> torch.Tensor:
+    """Recompute the Morton cube (box[6:8]) from box[0:6]."""
+    if is_gpu(box):
+        check(_native.hip().lsk_hip_box_finalize(_ptr(box), _stream(box)), "box_finalize")
+        return box
+    lo, hi = box[0:3], box[3:6]
+    ex = float(torch.max(hi - lo)) if bool(torch.all(torch.isfinite(box[0:6]))) else 0.0
+    ok = ex > 0 and math.isfinite(ex)
+    box[6] = 1024.0 / ex if ok else 0.0
+    box[7] = ex if ok else 0.0
+    return box
+
+
+# --------------------------------------------------------------------------- Morton + sort
+def morton(pts: torch.Tensor, box: torch.Tensor, with_iota: bool = True):
+    """30-bit Morton keys of pts in the cube of `box`; returns (keys, iota)."""
+    n = pts.shape[0]
+    keys = torch.empty(n, dtype=torch.int32, device=pts.device)
+    vals = torch.empty(n, dtype=torch.int32, device=pts.device) if with_iota else None
+    if is_gpu(pts):
+        check(_native.hip().lsk_hip_morton(_ptr(pts), n, _ptr(box), _ptr(keys), _ptr(vals), _stream(pts)),
+              "morton")
+        return keys, vals
+    b = box.detach().cpu()
+    origin = b[0:3].contiguous()
+    _native.host().lsk_cpu_morton(_ptr(pts.contiguous()), n, _ptr(origin), C.c_float(float(b[6])),
+                                  _ptr(keys), _nthreads())
+    if vals is not None:
+        vals.copy_(torch.arange(n, dtype=torch.int32))
+    return keys, vals
+
+
+def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, key_bits: int = 30):
+    """Stable sort of (key, value) int32 pairs by the low `key_bits` bits of key (unsigned)."""
+    n = keys.shape[0]
+    if not is_gpu(keys):
+        k64 = keys.to(torch.int64) & ((1 << 32) - 1)
+        if key_bits < 32:
+            k64 = k64 & ((1 << key_bits) - 1)
+        order = torch.sort(k64, stable=True).indices
+        return keys[order], vals[order]
+    lib = _native.hip()
+    ka = torch.empty_like(keys)
+    va = torch.empty_like(vals)
+    ws = torch.empty(lib.lsk_hip_sort_ws_bytes(n), dtype=torch.uint8, device=keys.device)
+    alt = C.c_int(0)
+    check(lib.lsk_hip_sort_pairs(_ptr(keys), _ptr(vals), _ptr(ka), _ptr(va), n, key_bits, _ptr(ws),
+                                 C.byref(alt), _stream(keys)), "sort_pairs")
+    return (ka, va) if alt.value else (keys, vals)
+
+
+def gather3(src: torch.Tensor, idx: torch.Tensor, pad: int = 0) -> torch.Tensor:
+    """dst[i] = src[idx[i]] for float3 rows; dst gets `pad` extra zero rows."""
+    n = idx.shape[0]
+    dst = torch.empty((n + pad, 3), dtype=torch.float32, device=src.device)
+    if pad:
+        dst[n:].zero_()
+    if is_gpu(src):
+        check(_native.hip().lsk_hip_gather3(_ptr(src), _ptr(idx), n, _ptr(dst), _stream(src)), "gather3")
+    else:
+        dst[:n] = src[idx.to(torch.int64)]
+    return dst
+
+
+def scatter1(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, finalize: bool) -> torch.Tensor:
+    """out[idx[i]] = f(src[i]) with f = sqrt-unless-inf when finalize."""
+    n = src.shape[0]
+    if is_gpu(src):
+        check(_native.hip().lsk_hip_scatter1(_ptr(src), _ptr(idx), n, _ptr(out), int(finalize), _stream(src)),
+              "scatter1")
+    else:
+        v = finalize_distances(src) if finalize else src
+        out[idx.to(torch.int64)] = v
+    return out
+
+
+def finalize_distances(d2: torch.Tensor) -> torch.Tensor:
+    """sqrt of the k-th squared distance unless it is +inf (reference extractFinalResult)."""
+    if is_gpu(d2):
+        out = torch.empty_like(d2)
+        check(_native.hip().lsk_hip_finalize(_ptr(d2), d2.shape[0], _ptr(out), _stream(d2)), "finalize")
+        return out
+    return torch.where(torch.isinf(d2), d2, torch.sqrt(d2))
+
+
+# --------------------------------------------------------------------------- tree
+def tree_depth(n: int) -> int:
+    nb = (n + BUCKET - 1) // BUCKET
+    d = 0
+    while (1 << d) < nb:
+        d += 1
+    return d
+
+
+def build_tree(sorted_pts: torch.Tensor, n: int) -> tuple[torch.Tensor, int]:
+    """Bucket tree over the first n rows of sorted_pts -> (nodes [2^(D+1), 8], depth)."""
+    depth = tree_depth(n)
+    slots = 1 << depth
+    if is_gpu(sorted_pts):
+        nodes = torch.empty((2 * slots, 8), dtype=torch.float32, device=sorted_pts.device)
+        check(_native.hip().lsk_hip_build_tree(_ptr(sorted_pts), n, _ptr(nodes), _stream(sorted_pts)),
+              "build_tree")
+        return nodes, depth
+    inf = float("inf")
+    lo = torch.full((slots * BUCKET, 3), inf)
+    hi = torch.full((slots * BUCKET, 3), -inf)
+    lo[:n] = sorted_pts[:n]
+    hi[:n] = sorted_pts[:n]
+    nodes = torch.zeros((2 * slots, 8), dtype=torch.float32)
+    nodes[slots:, 0:3] = lo.view(slots, BUCKET, 3).amin(dim=1)
+    nodes[slots:, 4:7] = hi.view(slots, BUCKET, 3).amax(dim=1)
+    for level in range(depth - 1, -1, -1):
+        a = 1 << level
+        ch = nodes[2 * a: 4 * a].view(a, 2, 8)
+        nodes[a:2 * a, 0:3] = torch.minimum(ch[:, 0, 0:3], ch[:, 1, 0:3])
+        nodes[a:2 * a, 4:7] = torch.maximum(ch[:, 0, 4:7], ch[:, 1, 4:7])
+        nodes[a:2 * a, 3] = torch.maximum(ch[:, 0, 3], ch[:, 1, 3])
+    return nodes, depth
+
+
+def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torch.Tensor:
+    """Store per-node max k-th squared radius (lo.w) of the queries below each node."""
+    if is_gpu(nodes):
+        check(_native.hip().lsk_hip_tree_set_radii(_ptr(nodes), n, _ptr(d2_sorted), _stream(nodes)),
+              "tree_set_radii")
+        return nodes
+    depth = tree_depth(n)
+    slots = 1 << depth
+    r = torch.zeros(slots * BUCKET, dtype=torch.float32)
+    r[:n] = d2_sorted[:n]
+    nodes[slots:, 3] = r.view(slots, BUCKET).amax(dim=1)
+    for level in range(depth - 1, -1, -1):
+        a = 1 << level
+        ch = nodes[2 * a: 4 * a].view(a, 2, 8)
+        nodes[a:2 * a, 3] = torch.maximum(ch[:, 0, 3], ch[:, 1, 3])
+    return nodes
+
+
+# --------------------------------------------------------------------------- kNN
+def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hint2: float,
+            out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
+            stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None) -> torch.Tensor:
+    """k-th squared distance for sorted queries against up to two bucket trees.
+
+    trees: list of (sorted_pts_padded, nodes, n, depth).
+    """
+    a = KnnArgs()
+    a.qpts = _ptr(qpts)
+    a.nq = nq
+    a.groups = _ptr(groups)
+    a.ngroups = ngroups
+    for i, (pts, nodes, n, depth) in enumerate(trees):
+        a.tree[i] = TreeView(_ptr(pts), _ptr(nodes), n, depth, 0)
+    a.ntrees = len(trees)
+    a.k = k
+    a.cut2 = cut2
+    a.r_hint2 = r_hint2
+    a.out_d2 = _ptr(out_d2)
+    a.stats = _ptr(stats)
+    a.qstatus = _ptr(qstatus)
+    check(_native.hip().lsk_hip_knn(C.byref(a), _stream(qpts)), "knn")
+    return out_d2
+
+
+def kth_cpu(points: torch.Tensor, queries: torch.Tensor, k: int, cut2: float, method: str = "kdtree") -> torch.Tensor:
+    """CPU oracle: k-th squared distance of each query among points (self counted if present)."""
+    pts = points.contiguous().float()
+    q = queries.contiguous().float()
+    out = torch.empty(q.shape[0], dtype=torch.float32)
+    f = _native.host().lsk_cpu_kth_kdtree if method == "kdtree" else _native.host().lsk_cpu_kth_brute
+    f(_ptr(pts), pts.shape[0], _ptr(q), q.shape[0], int(k), C.c_float(cut2), _ptr(out), _nthreads())
+    return out
+
+
+# --------------------------------------------------------------------------- halo
+def halo_mask(pts: torch.Tensor, pub: torch.Tensor, pub_off: list[int], pub_depth: list[int], self_rank: int) -> torch.Tensor:
+    """Per point bitmask of ranks whose published radius-inflated boxes contain it."""
+    n = pts.shape[0]
+    nranks = len(pub_off)
+    mask = torch.empty(n, dtype=torch.int64, device=pts.device)
+    if is_gpu(pts):
+        off = torch.tensor(pub_off, dtype=torch.int64, device=pts.device)
+        dep = torch.tensor(pub_depth, dtype=torch.int32, device=pts.device)
+        check(_native.hip().lsk_hip_halo_mask(_ptr(pts), n, _ptr(pub), _ptr(off), _ptr(dep), nranks,
+                                              self_rank, _ptr(mask), _stream(pts)), "halo_mask")
+        return mask
+    # CPU: test against the leaf level of each published tree
+    boxes, offs = [], [0]
+    for j in range(nranks):
+        d = pub_depth[j]
+        base = pub_off[j] // 8
+        leaves = pub[base + (1 << d): base + (2 << d)]
+        boxes.append(leaves)
+        offs.append(offs[-1] + leaves.shape[0])
+    allb = torch.cat(boxes).contiguous() if boxes else torch.zeros((0, 8))
+    offs_t = torch.tensor(offs, dtype=torch.int64)
+    _native.host().lsk_cpu_halo_mask(_ptr(pts.contiguous()), n, _ptr(allb), _ptr(offs_t), nranks, self_rank,
+                                     _ptr(mask), _nthreads())
+    return mask

@@ -1,0 +1,246 @@
+"""Communicator abstraction for the distributed pipelines.
+
+The reference talks CUDA-aware MPI directly (MPIComm + CUKD_MPI_CALL,
+unorderedDataVariant.cu:23-39; call-site inventory SURVEY §2.6). Here the pipelines
+talk to a small interface with the four collectives the k-NN exchange needs:
+
+* ``allreduce_(t, op)``      — in-place min / max / sum (bounds, histograms, flags)
+* ``allgather(t)``           — equal-size gather (published halo trees, counts)
+* ``alltoallv(send, counts)``— all-to-all-v of rows (spatial redistribution, halo
+                               exchange, result return)
+* ``barrier()``
+
+Implementations:
+
+* :class:`TorchComm` — one process per GPU over ``torch.distributed``; backend ``nccl``
+  is RCCL on ROCm (xGMI peer-to-peer), ``gloo`` for CPU tensors / tests.
+* :class:`LoopbackComm` — P virtual ranks as threads of one process sharing one device
+  (SURVEY §4.2 T3): lets every multi-rank pipeline run on a single GPU or on CPU.
+* :class:`SingleComm` — size 1.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Sequence
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    rank: int = 0
+    size: int = 1
+
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        """Returns a tensor of shape [size, *t.shape]."""
+        raise NotImplementedError
+
+    def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int]) -> tuple[torch.Tensor, list[int]]:
+        """Rows send[sum(counts[:j]) : sum(counts[:j+1])] go to rank j. Returns
+        (recv rows ordered by source rank, recv counts per source)."""
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    # convenience -----------------------------------------------------------------
+    def exchange_counts(self, send_counts: Sequence[int]) -> list[int]:
+        t = torch.tensor(list(send_counts), dtype=torch.int64)
+        allc = self.allgather_host(t)
+        return [int(allc[j, self.rank]) for j in range(self.size)]
+
+    def allgather_host(self, t: torch.Tensor) -> torch.Tensor:
+        """allgather of a small CPU tensor (moved to the comm device if needed)."""
+        return self.allgather(t.to(self.device)).cpu()
+
+    @property
+    def device(self) -> torch.device:
+        return torch.device("cpu")
+
+
+class SingleComm(Comm):
+    def __init__(self, device: torch.device | str = "cpu"):
+        self.rank, self.size = 0, 1
+        self._device = torch.device(device)
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    def allreduce_(self, t, op="sum"):
+        return t
+
+    def allgather(self, t):
+        return t.unsqueeze(0).clone()
+
+    def alltoallv(self, send, send_counts):
+        return send.clone(), [int(send_counts[0])]
+
+    def barrier(self):
+        pass
+
+
+_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+
+
+class TorchComm(Comm):
+    """torch.distributed process group (RCCL for GPU tensors, gloo for CPU)."""
+
+    def __init__(self, device: torch.device | str, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+        self._device = torch.device(device)
+        self.backend = dist.get_backend(group)
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    def allreduce_(self, t, op="sum"):
+        if self.size > 1:
+            dist.all_reduce(t, op=_OPS[op], group=self.group)
+        return t
+
+    def allgather(self, t):
+        t = t.contiguous()
+        out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
+        if self.size == 1:
+            out[0].copy_(t)
+        elif self.backend == "gloo":
+            dist.all_gather(list(out.unbind(0)), t, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
+    def alltoallv(self, send, send_counts):
+        send_counts = [int(c) for c in send_counts]
+        recv_counts = self.exchange_counts(send_counts)
+        row_shape = tuple(send.shape[1:])
+        recv = torch.empty((sum(recv_counts), *row_shape), dtype=send.dtype, device=send.device)
+        if self.size == 1:
+            recv.copy_(send)
+        else:
+            dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=recv_counts,
+                                   input_split_sizes=send_counts, group=self.group)
+        return recv, recv_counts
+
+    def barrier(self):
+        if self.size > 1:
+            if self.backend == "nccl":
+                # device barrier via a 1-element all-reduce keeps RCCL the only channel
+                t = torch.zeros(1, device=self._device)
+                dist.all_reduce(t, group=self.group)
+                torch.cuda.synchronize(self._device)
+            else:
+                dist.barrier(group=self.group)
+
+
+class _Hub:
+    def __init__(self, size: int):
+        self.size = size
+        self.barrier = threading.Barrier(size)
+        self.slots: list = [None] * size
+
+
+class LoopbackComm(Comm):
+    """P virtual ranks as threads of one process (tests; one GPU or CPU)."""
+
+    def __init__(self, hub: _Hub, rank: int, device: torch.device | str):
+        self.hub = hub
+        self.rank = rank
+        self.size = hub.size
+        self._device = torch.device(device)
+
+    @staticmethod
+    def create(size: int, device: torch.device | str = "cpu") -> list["LoopbackComm"]:
+        hub = _Hub(size)
+        return [LoopbackComm(hub, r, device) for r in range(size)]
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    def _sync_device(self):
+        if self._device.type == "cuda":
+            torch.cuda.current_stream(self._device).synchronize()
+
+    def _share(self, obj):
+        self._sync_device()
+        self.hub.slots[self.rank] = obj
+        self.hub.barrier.wait()
+        allv = list(self.hub.slots)
+        self.hub.barrier.wait()
+        return allv
+
+    def allreduce_(self, t, op="sum"):
+        allv = self._share(t.clone())
+        acc = allv[0].clone()
+        for v in allv[1:]:
+            v = v.to(acc.device)
+            if op == "sum":
+                acc += v
+            elif op == "min":
+                acc = torch.minimum(acc, v)
+            else:
+                acc = torch.maximum(acc, v)
+        t.copy_(acc)
+        self._sync_device()
+        return t
+
+    def allgather(self, t):
+        allv = self._share(t.clone())
+        out = torch.stack([v.to(t.device) for v in allv])
+        self._sync_device()
+        return out
+
+    def alltoallv(self, send, send_counts):
+        send_counts = [int(c) for c in send_counts]
+        offs = [0]
+        for c in send_counts:
+            offs.append(offs[-1] + c)
+        allv = self._share((send.clone(), offs))
+        parts, counts = [], []
+        for src in range(self.size):
+            s, o = allv[src]
+            parts.append(s[o[self.rank]:o[self.rank + 1]].to(send.device))
+            counts.append(o[self.rank + 1] - o[self.rank])
+        recv = torch.cat(parts) if parts else send[:0].clone()
+        self._sync_device()
+        return recv, counts
+
+    def barrier(self):
+        self._sync_device()
+        self.hub.barrier.wait()
+
+
+def run_loopback(size: int, fn, device: torch.device | str = "cpu"):
+    """Run fn(comm) on `size` virtual ranks (threads); returns the per-rank results."""
+    comms = LoopbackComm.create(size, device)
+    results: list = [None] * size
+    errors: list = [None] * size
+
+    def worker(r):
+        try:
+            if torch.device(device).type == "cuda":
+                torch.cuda.set_device(torch.device(device))
+            results[r] = fn(comms[r])
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errors[r] = e
+            comms[r].hub.barrier.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(size)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errors:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errors:
+        if e is not None:
+            raise e
+    return results

@@ -1,0 +1,292 @@
+"""Distributed k-th-NN distance pipelines (one rank per GPU).
+
+Fast path ("halo" mode), shared by both entrypoints:
+
+1. (unordered only) spatial redistribution — global bounds (all-reduce), 30-bit Morton
+   keys in the global cube, global histogram of the top 16 key bits (all-reduce) ->
+   P-1 balanced splitters, destination-rank partition (radix sort by rank), rows moved
+   with all-to-all-v. This is the sequence-parallel/Ulysses-style reshard of SURVEY §5.7a
+   and replaces the reference's P-round ring of whole trees (unorderedDataVariant.cu:
+   173-205, P kNN passes per query, O(P) traffic).
+2. local index (Morton sort + bucket tree) and local k-NN on the owned points.
+3. halo exchange — each rank publishes the top levels of its tree with per-node max
+   k-NN radius (all-gather, tiny); every rank sends exactly the points that fall
+   inside another rank's radius-inflated boxes (halo_mask kernel, all-to-all-v); the
+   receiver builds a halo tree and re-queries only the query groups that have a halo
+   point closer than their current k-th distance (2-tree k-NN kernel). Exact, because
+   local radii are upper bounds and the filter is conservative (halo.hip).
+   Replaces the bounds-culled whole-tree pulls of prePartitionedDataVariant.cu:304-357.
+4. (unordered only) distances return to the origin rank with the reverse all-to-all-v
+   and are scattered to input order.
+
+The reference-faithful schedules (ring rotation, peer pulls) live in ``refalgo.py``.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..models import knn_engine as E
+from ..ops import kernels as K
+from .comm import Comm
+
+SPLIT_BITS = 16  # splitter resolution: top 16 of the 30 Morton bits
+
+
+@dataclass
+class PhaseTimer:
+    """Per-phase wall times (device-synchronised when enabled)."""
+    enabled: bool = False
+    device: torch.device | None = None
+    times: dict = field(default_factory=dict)
+    _t: float = 0.0
+
+    def start(self):
+        if self.enabled:
+            self._sync()
+            self._t = time.perf_counter()
+
+    def mark(self, name: str):
+        if self.enabled:
+            self._sync()
+            now = time.perf_counter()
+            self.times[name] = self.times.get(name, 0.0) + (now - self._t)
+            self._t = now
+
+    def _sync(self):
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+
+@dataclass
+class RunInfo:
+    timer: PhaseTimer
+    stats: E.KnnStats = field(default_factory=E.KnnStats)
+    counts: dict = field(default_factory=dict)
+
+
+# --------------------------------------------------------------------------- helpers
+def global_box(points: torch.Tensor, comm: Comm) -> torch.Tensor:
+    box = K.bounds(points)
+    if comm.size > 1:
+        v = torch.cat([box[0:3], -box[3:6]])
+        comm.allreduce_(v, "min")
+        box = torch.cat([v[0:3], -v[3:6], box[6:8]])
+        box = K.box_finalize(box)
+    return box
+
+
+def _splitters(hist: torch.Tensor, total: int, size: int) -> list[int]:
+    """Bin starts of ranks 1..P-1 so that each rank owns ~total/P points."""
+    cum = torch.cumsum(hist.to(torch.int64), 0)
+    excl = torch.cat([torch.zeros(1, dtype=torch.int64), cum[:-1]])
+    out = []
+    for j in range(1, size):
+        target = (total * j) // size
+        b = int(torch.searchsorted(excl, torch.tensor([target], dtype=torch.int64), right=False)[0])
+        out.append(min(max(b, out[-1] if out else 0), hist.shape[0]))
+    return out
+
+
+def _dest_and_perm(keys: torch.Tensor, splitters: list[int], size: int):
+    n = keys.shape[0]
+    dev = keys.device
+    shift = 30 - SPLIT_BITS
+    if K.is_gpu(keys):
+        from .. import _native
+        lib = _native.hip()
+        split_t = torch.tensor(splitters if splitters else [0], dtype=torch.int32, device=dev)
+        dest = torch.empty(n, dtype=torch.int32, device=dev)
+        iota = torch.empty(n, dtype=torch.int32, device=dev)
+        K.check(lib.lsk_hip_dest_rank(keys.data_ptr(), n, split_t.data_ptr(), len(splitters), shift,
+                                      dest.data_ptr(), iota.data_ptr(), K._stream(keys)), "dest_rank")
+        counts = torch.zeros(size, dtype=torch.int32, device=dev)
+        K.check(lib.lsk_hip_count_dest(dest.data_ptr(), n, size, counts.data_ptr(), K._stream(keys)),
+                "count_dest")
+    else:
+        bins = (keys.to(torch.int64) >> shift)
+        split_t = torch.tensor(splitters, dtype=torch.int64)
+        dest = torch.searchsorted(split_t, bins, right=True).to(torch.int32)
+        iota = torch.arange(n, dtype=torch.int32)
+        counts = torch.bincount(dest.to(torch.int64), minlength=size).to(torch.int32)
+    bits = max(1, (size - 1).bit_length())
+    _, perm = K.sort_pairs(dest, iota, bits)
+    return perm, counts
+
+
+def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunInfo):
+    """Move every point to the rank owning its Morton range.
+    Returns (owned points, recv_counts, send permutation, send counts)."""
+    size = comm.size
+    keys, _ = K.morton(points, box, with_iota=False)
+    nb = 1 << SPLIT_BITS
+    hist = torch.zeros(nb, dtype=torch.int32, device=points.device)
+    if K.is_gpu(keys):
+        from .. import _native
+        K.check(_native.hip().lsk_hip_key_histogram(keys.data_ptr(), keys.shape[0], 30 - SPLIT_BITS,
+                                                   hist.data_ptr(), K._stream(keys)), "key_histogram")
+    else:
+        hist += torch.bincount((keys.to(torch.int64) >> (30 - SPLIT_BITS)), minlength=nb).to(torch.int32)
+    comm.allreduce_(hist, "sum")
+    hist_h = hist.cpu()
+    total = int(hist_h.to(torch.int64).sum())
+    splitters = _splitters(hist_h, total, size)
+    perm, counts = _dest_and_perm(keys, splitters, size)
+    send = K.gather3(points, perm)
+    send_counts = counts.cpu().tolist()
+    info.timer.mark("partition")
+    recv, recv_counts = comm.alltoallv(send, send_counts)
+    info.timer.mark("alltoallv_points")
+    info.counts["sent_points"] = sum(send_counts) - send_counts[comm.rank]
+    info.counts["owned_points"] = int(recv.shape[0])
+    return recv, recv_counts, perm, send_counts
+
+
+def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig, hint2: float,
+                info: RunInfo) -> torch.Tensor:
+    """Exchange boundary candidates and re-query the affected query groups (exact)."""
+    size, rank = comm.size, comm.rank
+    n = index.n
+    dev = index.device
+    levels = cfg.publish_levels
+    # 1. publish top levels of the radius-annotated tree
+    K.tree_set_radii(index.nodes, n, d2)
+    my_levels = min(levels, index.depth)
+    rows = 2 << levels
+    pub = torch.zeros((rows, 8), dtype=torch.float32, device=dev)
+    pub[:, 0:3] = math.inf
+    pub[:, 4:7] = -math.inf
+    take = min(rows, index.nodes.shape[0], 2 << my_levels)
+    pub[:take] = index.nodes[:take]
+    meta = torch.tensor([my_levels], dtype=torch.int32, device=dev)
+    pub_all = comm.allgather(pub)                       # [P, rows, 8]
+    depths = comm.allgather(meta).view(-1).cpu().tolist()
+    info.timer.mark("halo_publish")
+    # 2. filter and pack own points for every other rank
+    pts = index.pts[:n]
+    offs = [j * rows * 8 for j in range(size)]
+    mask = K.halo_mask(pts, pub_all.reshape(-1), offs, depths, rank)
+    if K.is_gpu(pts):
+        from .. import _native
+        lib = _native.hip()
+        counts = torch.zeros(size, dtype=torch.int32, device=dev)
+        K.check(lib.lsk_hip_mask_counts(mask.data_ptr(), n, size, counts.data_ptr(), K._stream(pts)),
+                "mask_counts")
+        send_counts = counts.cpu().tolist()
+        offsets = [0]
+        for c in send_counts:
+            offsets.append(offsets[-1] + c)
+        send = torch.empty((offsets[-1], 3), dtype=torch.float32, device=dev)
+        off_t = torch.tensor(offsets[:-1], dtype=torch.int64, device=dev)
+        cursors = torch.zeros(size, dtype=torch.int32, device=dev)
+        K.check(lib.lsk_hip_halo_pack(pts.data_ptr(), mask.data_ptr(), n, size, off_t.data_ptr(),
+                                      cursors.data_ptr(), send.data_ptr(), K._stream(pts)), "halo_pack")
+    else:
+        parts, send_counts = [], []
+        for j in range(size):
+            sel = ((mask >> j) & 1).bool()
+            parts.append(pts[sel])
+            send_counts.append(int(sel.sum()))
+        send = torch.cat(parts) if parts else pts[:0]
+    info.timer.mark("halo_filter")
+    recv, recv_counts = comm.alltoallv(send, send_counts)
+    info.counts["halo_sent"] = int(sum(send_counts))
+    info.counts["halo_recv"] = int(recv.shape[0])
+    info.timer.mark("halo_alltoallv")
+    nh = recv.shape[0]
+    if nh == 0 or n == 0:
+        return d2
+    # 3. halo tree, flag affected groups, re-query them against local + halo
+    hidx = E.build_index(recv)
+    if K.is_gpu(pts):
+        from .. import _native
+        lib = _native.hip()
+        ng = (n + 63) // 64
+        flags = torch.empty(ng, dtype=torch.int32, device=dev)
+        K.check(lib.lsk_hip_flag_query_groups(index.pts.data_ptr(), d2.data_ptr(), n, hidx.nodes.data_ptr(),
+                                              hidx.depth, nh, flags.data_ptr(), K._stream(pts)), "flag_groups")
+        glist = torch.empty(ng, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        K.check(lib.lsk_hip_compact_flags(flags.data_ptr(), ng, glist.data_ptr(), cnt.data_ptr(),
+                                          K._stream(pts)), "compact_flags")
+        nflag = int(cnt.item())
+        info.counts["requery_groups"] = nflag
+        info.timer.mark("halo_tree")
+        if nflag:
+            E.query(index, cfg, hint2, extra=hidx, groups=glist, ngroups=nflag, out=d2,
+                    stats=info.stats if cfg.collect_stats else None)
+    else:
+        info.timer.mark("halo_tree")
+        E.query(index, cfg, hint2, extra=hidx, out=d2)
+    info.timer.mark("halo_requery")
+    return d2
+
+
+# --------------------------------------------------------------------------- entrypoints
+def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
+                  n_total: int | None = None) -> torch.Tensor:
+    """k-th-NN distance of every local point (input order) for a globally unordered set
+    block-partitioned over ranks (reference unorderedData variant)."""
+    info = info or RunInfo(PhaseTimer(False, points.device))
+    info.timer.start()
+    points = points.contiguous()
+    n_local = points.shape[0]
+    if n_total is None:
+        t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
+        comm.allreduce_(t, "sum")
+        n_total = int(t.item())
+    box = global_box(points, comm)
+    hint2 = E.radius_hint2(box, n_total, cfg.k)
+    info.timer.mark("bounds")
+    if comm.size == 1:
+        index = E.build_index(points, box)
+        info.timer.mark("build")
+        d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
+        info.timer.mark("knn_local")
+        out = torch.empty(n_local, dtype=torch.float32, device=points.device)
+        K.scatter1(d2, index.perm, out, finalize=True)
+        info.timer.mark("return")
+        return out
+    owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
+    index = E.build_index(owned, box)
+    info.timer.mark("build")
+    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
+    info.timer.mark("knn_local")
+    d2 = halo_refine(index, d2, comm, cfg, hint2, info)
+    dist_owned = torch.empty(index.n, dtype=torch.float32, device=points.device)
+    K.scatter1(d2, index.perm, dist_owned, finalize=True)
+    back, _ = comm.alltoallv(dist_owned, recv_counts)
+    out = torch.empty(n_local, dtype=torch.float32, device=points.device)
+    K.scatter1(back, send_perm, out, finalize=False)
+    info.timer.mark("return")
+    return out
+
+
+def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
+                       info: RunInfo | None = None) -> torch.Tensor:
+    """k-th-NN distance of every local point (input order) when each rank holds one
+    (spatially coherent) input file (reference prePartitionedData variant)."""
+    info = info or RunInfo(PhaseTimer(False, points.device))
+    info.timer.start()
+    points = points.contiguous()
+    n_local = points.shape[0]
+    t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
+    comm.allreduce_(t, "sum")
+    n_total = int(t.item())
+    box = K.bounds(points)
+    gbox = global_box(points, comm)
+    hint2 = E.radius_hint2(gbox, n_total, cfg.k)
+    info.timer.mark("bounds")
+    index = E.build_index(points, box)
+    info.timer.mark("build")
+    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
+    info.timer.mark("knn_local")
+    if comm.size > 1:
+        d2 = halo_refine(index, d2, comm, cfg, hint2, info)
+    out = torch.empty(n_local, dtype=torch.float32, device=points.device)
+    K.scatter1(d2, index.perm, out, finalize=True)
+    info.timer.mark("return")
+    return out

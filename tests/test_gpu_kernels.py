@@ -1,0 +1,141 @@
+"""GPU numerics tests: every gfx950 kernel against a plain PyTorch / C++ CPU reference.
+
+The k-NN result must match the CPU oracle bit for bit (canonical dist² formula,
+correctly rounded sqrt), for every data distribution, k and cutoff.
+"""
+import math
+
+import pytest
+import torch
+
+from datasets import GENERATORS, lattice, uniform
+from mpi_cuda_largescaleknn_amd.models import knn_engine as E
+from mpi_cuda_largescaleknn_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def oracle(points, k, max_radius=math.inf, method="kdtree"):
+    d2 = K.kth_cpu(points, points, k, E.cut2_of(max_radius), method)
+    return K.finalize_distances(d2)
+
+
+def test_native_library_is_loaded():
+    from mpi_cuda_largescaleknn_amd import _native
+    lib = _native.hip()
+    assert lib.lsk_hip_abi_version() == 1
+    import ctypes as C
+    buf = C.create_string_buffer(512)
+    assert lib.lsk_hip_device_info(0, buf, 512) == 0
+    assert b"gfx950" in buf.value
+
+
+def test_bounds_matches_torch():
+    p = uniform(100003, seed=1).to(DEV) * 7 - 3
+    box = K.bounds(p).cpu()
+    assert torch.equal(box[0:3], p.min(0).values.cpu())
+    assert torch.equal(box[3:6], p.max(0).values.cpu())
+    ex = float((box[3:6] - box[0:3]).max())
+    assert box[6].item() == pytest.approx(1024.0 / ex)
+
+
+def test_morton_matches_cpu():
+    p = uniform(50000, seed=2)
+    box = K.bounds(p)
+    kc, _ = K.morton(p, box)
+    kg, iota = K.morton(p.to(DEV), box.to(DEV))
+    assert torch.equal(kc, kg.cpu())
+    assert torch.equal(iota.cpu(), torch.arange(50000, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 4095, 4096, 4097, 100000, 1000003])
+@pytest.mark.parametrize("bits", [8, 30])
+def test_radix_sort_matches_torch_stable_sort(n, bits):
+    g = torch.Generator().manual_seed(n)
+    keys = torch.randint(0, 1 << bits, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    vals = torch.arange(n, dtype=torch.int32)
+    ks, vs = K.sort_pairs(keys.to(DEV), vals.to(DEV), bits)
+    kr, vr = K.sort_pairs(keys, vals, bits)
+    assert torch.equal(ks.cpu(), kr)
+    assert torch.equal(vs.cpu(), vr)  # stability
+
+
+def test_radix_sort_full_32bit_keys():
+    n = 300000
+    g = torch.Generator().manual_seed(5)
+    keys = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    vals = torch.arange(n, dtype=torch.int32)
+    ks, vs = K.sort_pairs(keys.to(DEV), vals.to(DEV), 32)
+    kr, vr = K.sort_pairs(keys, vals, 32)
+    assert torch.equal(ks.cpu(), kr) and torch.equal(vs.cpu(), vr)
+
+
+@pytest.mark.parametrize("n", [1, 64, 65, 1000, 77777])
+def test_tree_build_matches_cpu(n):
+    p = uniform(n, seed=n)
+    idx = E.build_index(p)
+    ig = E.build_index(p.to(DEV))
+    assert torch.equal(ig.perm.cpu(), idx.perm)
+    assert torch.equal(ig.pts[:n].cpu(), idx.pts[:n])
+    assert ig.depth == idx.depth
+    assert torch.equal(ig.nodes.cpu()[1:], idx.nodes[1:])
+
+
+@pytest.mark.parametrize("dist", list(GENERATORS))
+@pytest.mark.parametrize("k", [1, 8, 16, 100])
+def test_knn_matches_oracle(dist, k):
+    p = GENERATORS[dist](30000, seed=k)
+    ref = oracle(p, k)
+    stats = E.KnnStats()
+    got = E.knn_distances(p.to(DEV), k, stats=stats).cpu()
+    bad = (got != ref) & ~(torch.isnan(got) & torch.isnan(ref))
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} mismatches; stats={stats.counters}"
+    assert stats.counters["mismatch_lanes"] == 0
+    assert stats.counters["pass_limit_waves"] == 0
+
+
+@pytest.mark.parametrize("k", [1, 5, 64, 100])
+def test_knn_cutoff(k):
+    p = uniform(20000, seed=3)
+    for r in [0.001, 0.02, 0.05, 1.0]:
+        ref = oracle(p, k, r)
+        got = E.knn_distances(p.to(DEV), k, max_radius=r).cpu()
+        assert torch.equal(got, ref), (k, r)
+
+
+def test_knn_k_larger_than_n_gives_inf():
+    p = uniform(50, seed=4)
+    got = E.knn_distances(p.to(DEV), 100).cpu()
+    assert torch.isinf(got).all()
+    got = E.knn_distances(p.to(DEV), 100, max_radius=0.25).cpu()
+    ref = oracle(p, 100, 0.25)
+    assert torch.equal(got, ref)
+
+
+def test_knn_edge_sizes():
+    for n in [1, 2, 3, 63, 64, 65, 127, 129]:
+        p = uniform(n, seed=n)
+        for k in [1, 2, n, n + 1]:
+            assert torch.equal(E.knn_distances(p.to(DEV), k).cpu(), oracle(p, k)), (n, k)
+
+
+def test_knn_all_identical_points():
+    p = torch.full((5000, 3), 0.25)
+    got = E.knn_distances(p.to(DEV), 100).cpu()
+    assert torch.equal(got, torch.zeros(5000))
+
+
+def test_knn_lattice_ties():
+    p = lattice(24)  # many exactly equal distances
+    for k in [1, 7, 27, 100]:
+        assert torch.equal(E.knn_distances(p.to(DEV), k).cpu(), oracle(p, k)), k
+
+
+def test_knn_large_uniform_brute_sample():
+    n = 2_000_000
+    p = uniform(n, seed=11)
+    got = E.knn_distances(p.to(DEV), 100).cpu()
+    idx = torch.randint(0, n, (2000,), generator=torch.Generator().manual_seed(1))
+    ref = K.finalize_distances(K.kth_cpu(p, p[idx], 100, math.inf, "brute"))
+    assert torch.equal(got[idx], ref)
