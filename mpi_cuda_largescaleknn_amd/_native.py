@@ -68,6 +68,8 @@ class KnnArgs(C.Structure):
         ("out_d2", vp),
         ("stats", vp),
         ("qstatus", vp),
+        ("seed", C.c_int32),
+        ("pad0", C.c_int32),
     ]
 
 

@@ -9,19 +9,23 @@
 // query. This kernel is designed for CDNA4 instead:
 //
 //  * A wavefront owns 64 consecutive Morton-sorted queries (= one tree bucket), so the
-//    traversal is wave-uniform: one LDS-resident node stack per wave, node boxes and
-//    candidate points are fetched with scalar loads (uniform addresses -> SGPRs) and
-//    every candidate costs the 64 lanes one VALU distance each — no divergence in the
-//    traversal and no LDS traffic for candidates.
+//    traversal is wave-uniform: one LDS-resident node stack per wave, node boxes come
+//    through scalar loads, and a leaf's 64 candidates are loaded with one vector load
+//    (prefetched one leaf ahead) and broadcast lane by lane with v_readlane — every
+//    candidate costs the 64 lanes one distance each, with no divergence and no LDS
+//    traffic for candidates.
 //  * Selection is a two-pass radix select on the bits of d² instead of a k-heap:
 //      pass 1 builds a per-lane 64-bin histogram (1/8-octave bins of d², 16-bit counts
-//             packed in LDS, lane-interleaved -> conflict-free ds_add_u32) and shrinks
-//             each lane's search radius online as soon as k candidates lie below a bin
-//             edge; afterwards the k-th value is known to lie in one narrow bin, with
-//             the exact count c_lo of smaller values;
-//      pass 2 replays the leaves visited in pass 1 (LDS leaf list), collects only the
-//             values inside that bin into a per-wave LDS pool, and each lane runs a
-//             (k-c_lo)-max-heap over its few collected values in LDS.
+//             packed in LDS, lane-interleaved -> conflict-free ds_add_u32, branch-free
+//             updates) and shrinks each lane's search radius as soon as k candidates
+//             lie below a bin edge; afterwards the k-th value lies in one narrow bin and
+//             the exact count c_lo of smaller values is known;
+//      pass 2 replays the leaves recorded in pass 1 (LDS leaf list) that cut some
+//             lane's shell [band_lo, band_hi), collects the values inside that bin into a
+//             per-wave LDS pool, and each lane runs a (k-c_lo)-max-heap over its few
+//             collected values in LDS.
+//    Pass 1 is seeded with the group's own bucket and its Morton neighbours, so most
+//    lanes start the tree walk with a radius close to the final one.
 //    Out-of-range estimates (under/overflow), oversized bins (refinement by 6 more bits)
 //    and duplicate-heavy data are handled by bounded extra passes, so the result is
 //    exact for any input: it equals the CPU oracle bit for bit.
@@ -37,14 +41,13 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 constexpr int kPool = 2048;      // dwords per wave: 32-dword histogram x 64 lanes, or collect pool
 constexpr int kStackCap = 64;    // DFS stack (depth <= 32 -> <= 33 live entries)
 constexpr int kLeafCap = 256;    // leaves recorded in pass 1 for replay
+constexpr int kBatch = 8;        // leaves gathered per processing batch
 constexpr int kBins = lsk::kSelBins;        // 64
 constexpr uint32_t kShift0 = 20;            // 1/8-octave bins of d²
 constexpr uint32_t kMaxPasses = 96;         // hard bound on passes per wave (never hang)
 
 enum : uint32_t { ST_HIST = 0, ST_READY = 1, ST_DONE = 2 };
 enum { MODE_HIST = 0, MODE_COLLECT = 1 };
-
-constexpr int kBatch = 8;        // leaves gathered per processing batch
 
 struct WaveLds {
   uint32_t pool[kPool];
@@ -59,7 +62,7 @@ struct Lane {
   // histogram pass state
   uint32_t lo_b, hi_b, shift;
   int32_t bin_hi;
-  uint32_t c_hi, top_cnt, zc;
+  uint32_t c_hi, zc;
   uint32_t cut_lim;  // min(cut2 bits, +inf bits)
   // band state (READY)
   uint32_t band_lo, band_w, m, bc;
@@ -75,23 +78,27 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
   s.hi_b = (uint32_t)hi;
   s.bin_hi = hi > lo_b ? (int32_t)((hi - lo_b + ((1ull << shift) - 1)) >> shift) : 0;
   s.c_hi = 0;
-  s.top_cnt = 0;
   s.zc = 0;
+}
+
+__device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
+  return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
+}
+
+// Count in the current top bin (the underflow bin once every bin is dropped).
+__device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *pool, int lane) {
+  return s.bin_hi > 0 ? hist_read(pool, (uint32_t)s.bin_hi - 1u, lane) : s.c_hi;
 }
 
 // Drop top bins while the bins below them already hold >= k values: every value in a
 // dropped bin is beyond the k-th, so the lane's search radius shrinks to that edge.
-__device__ __forceinline__ void hist_shrink(Lane &s, uint32_t *pool, int lane, uint32_t k) {
-  while (s.c_hi - s.top_cnt >= k) {
-    s.c_hi -= s.top_cnt;
+__device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
+  while (s.bin_hi > 0) {
+    const uint32_t top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
+    if (s.c_hi - top < k) break;
+    s.c_hi -= top;
     s.bin_hi--;
     s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
-    if (s.bin_hi > 0) {
-      const uint32_t bb = (uint32_t)s.bin_hi - 1u;
-      s.top_cnt = (pool[(bb >> 1) * lsk::kWave + lane] >> ((bb & 1u) << 4)) & 0xffffu;
-    } else {
-      s.top_cnt = s.c_hi;  // the underflow bin is now the top
-    }
   }
 }
 
@@ -102,7 +109,7 @@ __device__ __forceinline__ float bcast(float v, uint32_t j) {
 // One leaf: lane j holds candidate j in (px,py,pz); candidates are broadcast with
 // v_readlane (no LDS traffic) and processed in chunks of 8. Histogram updates are
 // branch-free (a lane that does not count a value adds 0 to a valid bin).
-template <int MODE>
+template <int MODE, bool ZC>
 __device__ __forceinline__ void process_points(Lane &s, float px, float py, float pz,
                                                uint32_t cnt, uint32_t *pool, int lane,
                                                uint32_t k) {
@@ -119,7 +126,6 @@ __device__ __forceinline__ void process_points(Lane &s, float px, float py, floa
     if (MODE == MODE_HIST) {
       if (!__ballot(umin < s.hi_b)) continue;
       const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift;
-      const uint32_t tlo = s.bin_hi > 0 ? lb + ((uint32_t)(s.bin_hi - 1) << sh) : 0u;
 #pragma unroll
       for (int t = 0; t < 8; t++) {
         const uint32_t v = u[t];
@@ -128,16 +134,14 @@ __device__ __forceinline__ void process_points(Lane &s, float px, float py, floa
         const uint32_t inc = (in && v >= lb) ? (1u << ((b & 1u) << 4)) : 0u;
         atomicAdd(&pool[(b >> 1) * lsk::kWave + lane], inc);
         s.c_hi += in ? 1u : 0u;
-        s.top_cnt += (in && v >= tlo) ? 1u : 0u;
-        s.zc += (v == 0u) ? 1u : 0u;
+        if (ZC) s.zc += (v == 0u) ? 1u : 0u;
       }
-      if (__ballot(s.c_hi - s.top_cnt >= k)) hist_shrink(s, pool, lane, k);
     } else {
       const uint32_t bl = s.band_lo, bw = s.band_w;
-      if (!__ballot(umin - bl < bw || (u[0] - bl < bw) || (u[1] - bl < bw) || (u[2] - bl < bw) ||
-                    (u[3] - bl < bw) || (u[4] - bl < bw) || (u[5] - bl < bw) || (u[6] - bl < bw) ||
-                    (u[7] - bl < bw)))
-        continue;
+      bool any = false;
+#pragma unroll
+      for (int t = 0; t < 8; t++) any = any || (u[t] - bl < bw);
+      if (!__ballot(any)) continue;
 #pragma unroll
       for (int t = 0; t < 8; t++) {
         if (u[t] - bl < bw) {
@@ -147,6 +151,8 @@ __device__ __forceinline__ void process_points(Lane &s, float px, float py, floa
       }
     }
   }
+  // one shrink check per leaf (the bound lags at most 64 candidates behind)
+  if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) hist_shrink(s, pool, lane, k);
 }
 
 __device__ __forceinline__ float lane_bound(const Lane &s, int mode) {
@@ -157,9 +163,12 @@ struct WaveCtx {
   WaveLds *L;
   int lane;
   uint32_t k;
-  float cx, cy, cz;   // group centre (near-first ordering)
+  uint32_t g;          // group id (== tree-0 bucket when queries are tree 0's points)
+  int32_t seed;        // neighbour buckets seeded on each side (0 = off)
+  float cx, cy, cz;    // group centre (near-first ordering)
   uint32_t nleaves;
   bool list_ok;
+  bool count_zero;     // count exact zeros (only after an underflow)
   uint32_t evals, leaves_visited, nodes_visited;
 };
 
@@ -192,7 +201,10 @@ __device__ void process_batch(Lane &s, WaveCtx &W, const lsk_knn_args &A, uint32
     if (i + 1 < nb) cnt = load_leaf(A, lsk::uniform(W.L->batch[i + 1]), W.lane, px, py, pz);
     W.leaves_visited++;
     W.evals += ccnt;
-    process_points<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+    if (MODE == MODE_HIST && W.count_zero)
+      process_points<MODE, true>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+    else
+      process_points<MODE, false>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
   }
 }
 
@@ -209,8 +221,24 @@ __device__ __forceinline__ void batch_push(WaveCtx &W, uint32_t &nb, uint32_t e,
   }
 }
 
+// Leaf test per lane. HIST: box closer than the lane's radius. COLLECT: the box cuts
+// the lane's shell [band_lo, band_hi) — a box entirely inside band_lo holds only values
+// already counted in c_lo (max-distance is monotone like box_dist2, common.h).
+template <int MODE>
+__device__ __forceinline__ bool leaf_needed(const Lane &s, const lsk::v4f &lo, const lsk::v4f &hi) {
+  const lsk::vec3f q{s.qx, s.qy, s.qz};
+  const bool near = lsk::box_dist2(q, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}) < lane_bound(s, MODE);
+  if (MODE == MODE_HIST) return near;
+  const float fx = fmaxf(fabsf(lo.x - s.qx), fabsf(hi.x - s.qx));
+  const float fy = fmaxf(fabsf(lo.y - s.qy), fabsf(hi.y - s.qy));
+  const float fz = fmaxf(fabsf(lo.z - s.qz), fabsf(hi.z - s.qz));
+  return near && fbits(lsk::dist2(fx, fy, fz)) >= s.band_lo;
+}
+
 // Depth-first, near-child-first walk of every tree with a per-wave LDS stack; needed
 // leaves are gathered into batches of kBatch and processed with load prefetching.
+// With seeding, tree 0's buckets [g-seed, g+seed] are processed first (nearest first)
+// and skipped by the walk.
 template <int MODE>
 __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A, bool record) {
   const lsk::vec3f q{s.qx, s.qy, s.qz};
@@ -221,6 +249,24 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A, bool record
     lsk::cfloat4_p nodes = lsk::as_const4(T.nodes);
     const uint32_t leaf0 = 1u << T.depth;
     const uint32_t nbuckets = (uint32_t)((T.n + lsk::kBucket - 1) / lsk::kBucket);
+    int64_t skip_lo = 1, skip_hi = 0;  // empty
+    if (t == 0 && W.seed > 0) {
+      skip_lo = (int64_t)W.g - W.seed;
+      skip_hi = (int64_t)W.g + W.seed;
+      uint32_t nb = 0;
+      for (int32_t d = 0; d <= W.seed; d++) {
+        for (int32_t sgn = 0; sgn < (d ? 2 : 1); sgn++) {
+          const int64_t b = sgn ? (int64_t)W.g + d : (int64_t)W.g - d;
+          if (b < 0 || b >= (int64_t)nbuckets) continue;
+          batch_push(W, nb, (uint32_t)b, record);
+          if (nb == (uint32_t)kBatch) {
+            process_batch<MODE>(s, W, A, nb);
+            nb = 0;
+          }
+        }
+      }
+      if (nb) process_batch<MODE>(s, W, A, nb);
+    }
     uint32_t sp = 0;
     if (W.lane == 0) W.L->stack[0] = 1u;
     sp = 1;
@@ -230,13 +276,16 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A, bool record
       while (sp > 0 && nb < (uint32_t)kBatch) {
         sp--;
         const uint32_t node = lsk::uniform(W.L->stack[sp]);
-        const lsk::v4f lo = nodes[2 * node], hi = nodes[2 * node + 1];
         W.nodes_visited++;
-        if (!__ballot(lsk::box_dist2(q, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}) < lim)) continue;
         if (node >= leaf0) {
-          if (node - leaf0 < nbuckets) batch_push(W, nb, (t << 31) | (node - leaf0), record);
+          const uint32_t b = node - leaf0;
+          if (b >= nbuckets || ((int64_t)b >= skip_lo && (int64_t)b <= skip_hi)) continue;
+          const lsk::v4f lo = nodes[2 * node], hi = nodes[2 * node + 1];
+          if (__ballot(leaf_needed<MODE>(s, lo, hi))) batch_push(W, nb, (t << 31) | b, record);
           continue;
         }
+        const lsk::v4f lo = nodes[2 * node], hi = nodes[2 * node + 1];
+        if (!__ballot(lsk::box_dist2(q, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}) < lim)) continue;
         const uint32_t c0 = 2 * node, c1 = c0 + 1;
         const lsk::v4f l0 = nodes[2 * c0], h0 = nodes[2 * c0 + 1];
         const lsk::v4f l1 = nodes[2 * c1], h1 = nodes[2 * c1 + 1];
@@ -265,19 +314,16 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A, bool record
 // lane's bound is <= its pass-1 bound).
 template <int MODE>
 __device__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
-  const lsk::vec3f q{s.qx, s.qy, s.qz};
   uint32_t i = 0;
   while (i < W.nleaves) {
     uint32_t nb = 0;
-    const float lim = lane_bound(s, MODE);
     for (; i < W.nleaves && nb < (uint32_t)kBatch; i++) {
       const uint32_t e = lsk::uniform(W.L->leaves[i]);
       const lsk_tree_view T = pick_tree(A, e >> 31);
       lsk::cfloat4_p nodes = lsk::as_const4(T.nodes);
       const uint32_t node = (1u << T.depth) + (e & 0x7fffffffu);
       const lsk::v4f lo = nodes[2 * node], hi = nodes[2 * node + 1];
-      if (__ballot(lsk::box_dist2(q, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}) < lim))
-        batch_push(W, nb, e, false);
+      if (__ballot(leaf_needed<MODE>(s, lo, hi))) batch_push(W, nb, e, false);
     }
     if (nb) process_batch<MODE>(s, W, A, nb);
   }
@@ -298,8 +344,8 @@ __device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
 }
 
 // Per-lane estimate of the k-th squared distance from the group's own points (pass 0):
-// the m0-th smallest squared distance to the 64 queries of the group (self included),
-// scaled by (k/m0)^(2/3) (uniform local density).
+// the m0-th smallest squared distance to the group's queries (self included, broadcast
+// from the lanes that hold them), scaled by (k/m0)^(2/3) (uniform local density).
 __device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k) {
   constexpr int M = 8;
   float best[M];
@@ -351,8 +397,11 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
   W.L = &lds[wid];
   W.lane = lane;
   W.k = k;
+  W.g = g;
+  W.seed = A.seed;
   W.nleaves = 0;
   W.list_ok = true;
+  W.count_zero = false;
   W.evals = W.leaves_visited = W.nodes_visited = 0;
 
   Lane s;
@@ -423,8 +472,9 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
       if (first || !W.list_ok) traverse<MODE_HIST>(s, W, A, first);
       else replay<MODE_HIST>(s, W, A);
       first = false;
-      bool ovf = false;
+      bool ovf = false, udf = false;
       if (s.state == ST_HIST) {
+        const uint32_t top = top_count(s, W.L->pool, lane);
         if (s.c_hi < k) {
           if (s.hi_b >= s.cut_lim) {
             s.state = ST_DONE;
@@ -436,14 +486,15 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
             set_range(s, s.hi_b, kShift0, s.cut_lim);
           }
         } else if (s.bin_hi == 0) {
-          if (s.zc >= k) {
+          if (W.count_zero && s.zc >= k) {
             s.state = ST_DONE;
             s.ans = 0u;
             qs |= QS_DONE_ZERO;
-          } else {  // estimate too large: next 8 octaves down
+          } else {  // estimate too large: next 8 octaves down, counting exact zeros
+            udf = true;
             qs |= QS_UNDERFLOW;
-            const uint32_t top = s.lo_b;
-            set_range(s, top > (64u << kShift0) ? top - (64u << kShift0) : 0u, kShift0, top);
+            const uint32_t topb = s.lo_b;
+            set_range(s, topb > (64u << kShift0) ? topb - (64u << kShift0) : 0u, kShift0, topb);
           }
         } else {
           const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
@@ -456,12 +507,13 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
             s.state = ST_READY;
             s.band_lo = bl;
             s.band_w = bw;
-            s.m = k - (s.c_hi - s.top_cnt);
-            s.bc = s.top_cnt;
+            s.m = k - (s.c_hi - top);
+            s.bc = top;
           }
         }
       }
       if (__ballot(ovf)) W.list_ok = false;
+      if (__ballot(udf)) W.count_zero = true;
     }
     if (limit) break;
     // carve the collect pool; refine the biggest bands if it does not fit
@@ -550,8 +602,8 @@ extern "C" int lsk_hip_knn(const lsk_knn_args *args, void *stream) {
     lsk::set_last_error("knn: k must be in [1, 65535] for the radix-select kernel");
     return 1;
   }
-  if (A.nq >= ((int64_t)1 << 32) || A.ntrees < 0 || A.ntrees > 2) {
-    lsk::set_last_error("knn: nq must be < 2^32 and ntrees in [0,2]");
+  if (A.nq >= ((int64_t)1 << 32) || A.ntrees < 0 || A.ntrees > 2 || A.seed < 0 || A.seed > 64) {
+    lsk::set_last_error("knn: nq must be < 2^32, ntrees in [0,2], seed in [0,64]");
     return 1;
   }
   for (int t = 0; t < A.ntrees; t++) {

@@ -88,6 +88,9 @@ typedef struct lsk_knn_args {
   float *out_d2;            // [nq] k-th squared distance per query (sorted order)
   unsigned long long *stats;  // optional [16] 64-bit counters (NULL = off)
   uint32_t *qstatus;        // optional [nq] per-query status bits (NULL = off)
+  int32_t seed;             // queries are tree[0]'s points: seed pass 1 with buckets
+                            // [g-seed, g+seed] of tree 0 (0 = off)
+  int32_t pad0;
 } lsk_knn_args;
 
 int lsk_hip_knn(const lsk_knn_args *args, void *stream);

@@ -29,6 +29,9 @@ def cut2_of(max_radius: float) -> float:
         return float(r * r)
 
 
+SEED_BUCKETS = 2  # Morton-neighbour buckets (each side) that seed the first pass
+
+
 @dataclass
 class KnnConfig:
     k: int
@@ -117,7 +120,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalInd
         trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
         raw = torch.zeros(16, dtype=torch.int64, device=index.device) if stats is not None else None
         K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
-                  stats=raw, qstatus=qstatus)
+                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS)
         if stats is not None:
             stats.add(raw)
         return out

@@ -136,7 +136,9 @@ def finalize_distances(d2: torch.Tensor) -> torch.Tensor:
         out = torch.empty_like(d2)
         check(_native.hip().lsk_hip_finalize(_ptr(d2), d2.shape[0], _ptr(out), _stream(d2)), "finalize")
         return out
-    return torch.where(torch.isinf(d2), d2, torch.sqrt(d2))
+    # torch's float32 CPU sqrt is not correctly rounded (vectorised approximation);
+    # sqrt in float64 then one rounding to float32 is (IEEE sqrtf, as on the GPU).
+    return torch.where(torch.isinf(d2), d2, torch.sqrt(d2.double()).float())
 
 
 # --------------------------------------------------------------------------- tree
@@ -195,10 +197,12 @@ def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torc
 # --------------------------------------------------------------------------- kNN
 def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hint2: float,
             out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
-            stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None) -> torch.Tensor:
+            stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
+            seed: int = 0) -> torch.Tensor:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
-    trees: list of (sorted_pts_padded, nodes, n, depth).
+    trees: list of (sorted_pts_padded, nodes, n, depth). seed > 0 declares that the
+    queries are trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
     """
     a = KnnArgs()
     a.qpts = _ptr(qpts)
@@ -214,6 +218,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     a.out_d2 = _ptr(out_d2)
     a.stats = _ptr(stats)
     a.qstatus = _ptr(qstatus)
+    a.seed = seed
     check(_native.hip().lsk_hip_knn(C.byref(a), _stream(qpts)), "knn")
     return out_d2
 
@@ -242,6 +247,7 @@ def halo_mask(pts: torch.Tensor, pub: torch.Tensor, pub_off: list[int], pub_dept
         return mask
     # CPU: test against the leaf level of each published tree
     boxes, offs = [], [0]
+    pub = pub.reshape(-1, 8)
     for j in range(nranks):
         d = pub_depth[j]
         base = pub_off[j] // 8
