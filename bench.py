@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm  # noqa: E402
 
 METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
@@ -43,6 +44,8 @@ def parse():
     ap.add_argument("--points", type=float, default=1e9)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--variant", choices=["unordered", "prepartitioned"], default="unordered")
+    ap.add_argument("--mode", choices=["halo", "ring", "peer"], default="halo",
+                    help="halo = MI355X pipeline; ring/peer = reference algorithm (ref-algo baseline)")
     ap.add_argument("--phases", action="store_true", help="print per-phase times (adds syncs)")
     ap.add_argument("--stats", action="store_true", help="collect k-NN kernel counters")
     return ap.parse_args()
@@ -92,7 +95,11 @@ def main():
         nonlocal info_last
         info = PL.RunInfo(PL.PhaseTimer(args.phases, device))
         pts = host_pts.to(device, non_blocking=True)
-        if args.variant == "unordered":
+        if args.mode == "ring":
+            out = RA.ring_knn(pts, comm, cfg, info)
+        elif args.mode == "peer":
+            out = RA.peer_knn(pts, comm, cfg, info)
+        elif args.variant == "unordered":
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total)
         else:
             out = PL.prepartitioned_knn(pts, comm, cfg, info)
@@ -139,8 +146,9 @@ def main():
                 "model": f"{args.variant}Data k-th-NN distance, k={args.k}",
                 "global_batch": n_total,
                 "seq_len": None,
-                "parallelism": f"spatial-redistribute+halo x{world}" if args.variant == "unordered"
-                else f"halo x{world}",
+                "parallelism": (f"ref-algo {args.mode} x{world}" if args.mode != "halo" else
+                                f"spatial-redistribute+halo x{world}" if args.variant == "unordered"
+                                else f"halo x{world}"),
                 "k": args.k,
                 "all_finite": finite,
             },

@@ -101,6 +101,12 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.lsk_cpu_morton.restype = None
     lib.lsk_cpu_halo_mask.argtypes = [vp, i64, vp, vp, i32, i32, vp, i32]
     lib.lsk_cpu_halo_mask.restype = None
+    lib.lsk_cpu_lbt_build.argtypes = [vp, i64, vp, vp]
+    lib.lsk_cpu_lbt_build.restype = None
+    lib.lsk_cpu_refalgo_knn.argtypes = [vp, i64, vp, i64, vp, i32, C.c_float, i32, vp, C.c_uint32, i32]
+    lib.lsk_cpu_refalgo_knn.restype = None
+    lib.lsk_cpu_refalgo_extract.argtypes = [vp, i64, i32, vp]
+    lib.lsk_cpu_refalgo_extract.restype = None
 
 
 def _declare_hip(lib: C.CDLL) -> None:
@@ -131,6 +137,11 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_compact_flags": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_halo_pack": ([vp, vp, i64, i32, vp, vp, vp, vp], i32),
         "lsk_hip_mask_counts": ([vp, i64, i32, vp, vp], i32),
+        "lsk_hip_lbt_keys": ([vp, i64, i32, vp, vp, vp], i32),
+        "lsk_hip_lbt_retag": ([vp, i64, i32, vp], i32),
+        "lsk_hip_gather_u32": ([vp, vp, i64, vp, vp], i32),
+        "lsk_hip_refalgo_knn": ([vp, i64, vp, i64, vp, i32, C.c_float, i32, vp, C.c_uint32, vp], i32),
+        "lsk_hip_refalgo_extract": ([vp, i64, i32, vp, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

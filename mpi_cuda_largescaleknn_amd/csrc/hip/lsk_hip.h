@@ -118,6 +118,22 @@ int lsk_hip_halo_pack(const float *pts, const uint64_t *mask, int64_t n, int nra
 int lsk_hip_mask_counts(const uint64_t *mask, int64_t n, int nranks, uint32_t *counts,
                         void *stream);
 
+// ---- ref-algo (reference algorithm baseline, refalgo.hip) -----------------------------
+// Sortable bits of coord[dim] -> keys, iota -> vals.
+int lsk_hip_lbt_keys(const float *pts, int64_t n, int dim, uint32_t *keys, uint32_t *vals,
+                     void *stream);
+// Tag update of the left-balanced builder for `level` (points sorted by (tag, coord)).
+int lsk_hip_lbt_retag(uint32_t *tags, int64_t n, int level, void *stream);
+int lsk_hip_gather_u32(const uint32_t *src, const uint32_t *idx, int64_t n, uint32_t *dst,
+                       void *stream);
+// runQuery: stack-free traversal of a left-balanced tree, global AoS k-max-heaps.
+int lsk_hip_refalgo_knn(const float *tree, int64_t n, const float *qpts, int64_t nq,
+                        unsigned long long *heaps, int k, float cut2, int init, float *rmax,
+                        uint32_t id_base, void *stream);
+// extractFinalResult
+int lsk_hip_refalgo_extract(const unsigned long long *heaps, int64_t nq, int k, float *out,
+                            void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,6 +90,17 @@ void lsk_cpu_halo_mask(const float *pts, int64_t n, const float *boxes,
                        const int64_t *box_offsets, int nsets, int skip_set,
                        uint64_t *mask, int nthreads);
 
+// ---------------------------------------------------------------- ref-algo (CPU twin)
+// Left-balanced k-d tree (object median, round-robin axis): out_pts in tree order,
+// out_ids[i] = input index of tree node i (may be NULL).
+void lsk_cpu_lbt_build(const float *pts, int64_t n, float *out_pts, uint32_t *out_ids);
+// Stack-free traversal + persisted k-max-heaps (AoS [nq][k] of d2bits<<32|id); init=1
+// (re)initialises with cut2; rmax (optional) receives max(rmax, max_q sqrt(top_q)).
+void lsk_cpu_refalgo_knn(const float *tree, int64_t n, const float *qpts, int64_t nq,
+                         unsigned long long *heaps, int k, float cut2, int init, float *rmax,
+                         uint32_t id_base, int nthreads);
+void lsk_cpu_refalgo_extract(const unsigned long long *heaps, int64_t nq, int k, float *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,13 @@ class Comm:
     def barrier(self) -> None:
         raise NotImplementedError
 
+    def p2p(self, sends: Sequence[tuple[int, torch.Tensor]],
+            recvs: Sequence[tuple[int, tuple, torch.dtype]]) -> list[torch.Tensor]:
+        """Grouped point-to-point exchange (the reference's Isend/Irecv/Waitall,
+        unorderedDataVariant.cu:183-193, prePartitionedDataVariant.cu:326-345):
+        sends = [(dst, tensor)], recvs = [(src, shape, dtype)] -> received tensors."""
+        raise NotImplementedError
+
     # convenience -----------------------------------------------------------------
     def exchange_counts(self, send_counts: Sequence[int]) -> list[int]:
         t = torch.tensor(list(send_counts), dtype=torch.int64)
@@ -81,6 +88,10 @@ class SingleComm(Comm):
 
     def barrier(self):
         pass
+
+    def p2p(self, sends, recvs):
+        box = {dst: t for dst, t in sends}
+        return [box[src].clone() for src, _, _ in recvs]
 
 
 _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
@@ -127,6 +138,20 @@ class TorchComm(Comm):
             dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=recv_counts,
                                    input_split_sizes=send_counts, group=self.group)
         return recv, recv_counts
+
+    def p2p(self, sends, recvs):
+        out = [torch.empty(shape, dtype=dt, device=self._device) for _, shape, dt in recvs]
+        ops = [dist.P2POp(dist.isend, t.contiguous(), dst, group=self.group) for dst, t in sends if dst != self.rank]
+        ops += [dist.P2POp(dist.irecv, buf, src, group=self.group)
+                for (src, _, _), buf in zip(recvs, out) if src != self.rank]
+        own = {dst: t for dst, t in sends if dst == self.rank}
+        for (src, _, _), buf in zip(recvs, out):
+            if src == self.rank:
+                buf.copy_(own[src])
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return out
 
     def barrier(self):
         if self.size > 1:
@@ -215,6 +240,12 @@ class LoopbackComm(Comm):
     def barrier(self):
         self._sync_device()
         self.hub.barrier.wait()
+
+    def p2p(self, sends, recvs):
+        allv = self._share({dst: t.clone() for dst, t in sends})
+        out = [allv[src][self.rank].to(self._device) for src, _, _ in recvs]
+        self._sync_device()
+        return out
 
 
 def run_loopback(size: int, fn, device: torch.device | str = "cpu"):

@@ -1,0 +1,111 @@
+"""Reference-faithful distributed schedules ("--mode ring" / "--mode peer").
+
+These reproduce the reference's communication structure on top of the ref-algo kernels
+(ops/refalgo.py) — they are the measured baseline of BASELINE.md and a fidelity check,
+not the fast path (pipelines.py):
+
+* ``ring_knn`` — unorderedData variant (unorderedDataVariant.cu:173-205):
+  every rank builds a left-balanced tree over its block of the file; queries stay put
+  while trees rotate rank -> rank+1 for P-1 rounds (count exchange, then payload, as
+  grouped point-to-point sends over RCCL); each round resumes every query's persisted
+  k-heap.
+* ``peer_knn`` — prePartitionedData variant (prePartitionedDataVariant.cu:284-357, S3):
+  rank AABBs and counts are all-gathered; each round every rank pulls at most one unseen
+  peer tree — the closest by box gap among peers closer than its current max k-NN
+  radius (Sattolo tie-break permutation) — and serves its own tree to every requester;
+  the job ends when every request is -1.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from ..models import knn_engine as E
+from ..ops import kernels as K
+from ..ops import refalgo as R
+from .comm import Comm
+from .pipelines import PhaseTimer, RunInfo
+
+
+def ring_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None) -> torch.Tensor:
+    info = info or RunInfo(PhaseTimer(False, points.device))
+    info.timer.start()
+    points = points.contiguous()
+    n = points.shape[0]
+    dev = points.device
+    tree, _ = R.build_lbt(points)
+    info.timer.mark("build")
+    heaps = R.alloc_heaps(n, cfg.k, dev)
+    nxt, prv = (comm.rank + 1) % comm.size, (comm.rank - 1 + comm.size) % comm.size
+    cur, cur_n = tree, n
+    for rnd in range(comm.size):
+        if rnd > 0:
+            cnt = torch.tensor([cur_n], dtype=torch.int64, device=comm.device)
+            (rc,) = comm.p2p([(nxt, cnt)], [(prv, (1,), torch.int64)])
+            recv_n = int(rc.item())
+            (cur,) = comm.p2p([(nxt, cur[:cur_n])], [(prv, (recv_n, 3), torch.float32)])
+            cur_n = recv_n
+            info.timer.mark("ring_exchange")
+        R.run_query(cur, cur_n, points, heaps, cfg.k, cfg.cut2, init=(rnd == 0))
+        info.timer.mark("knn_rounds")
+    out = R.extract(heaps, n, cfg.k)
+    info.timer.mark("return")
+    return out
+
+
+def peer_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
+             log=None) -> torch.Tensor:
+    info = info or RunInfo(PhaseTimer(False, points.device))
+    info.timer.start()
+    points = points.contiguous()
+    n = points.shape[0]
+    dev = points.device
+    size, me = comm.size, comm.rank
+    host = _native.host()
+    box = K.bounds(points)[0:6].float().cpu().contiguous()
+    all_boxes = comm.allgather(box.to(comm.device)).cpu().contiguous()          # [P, 6]
+    counts = comm.allgather(torch.tensor([n], dtype=torch.int64, device=comm.device)).view(-1).cpu().tolist()
+    perm = (torch.zeros(size, dtype=torch.int32)).contiguous()
+    host.lsk_peer_permutation(me, size, perm.data_ptr())
+    my_tree, _ = R.build_lbt(points)
+    info.timer.mark("build")
+    heaps = R.alloc_heaps(n, cfg.k, dev)
+    rmax = torch.zeros(1, dtype=torch.float32, device=dev)
+    seen = torch.zeros(size, dtype=torch.uint8)
+    initialised = False
+    for rnd in range(size):
+        comm.barrier()
+        if me == 0 and log is not None:
+            log(f"round {rnd}")
+        if rnd == 0:
+            work, wn = my_tree, n
+            seen[me] = 1
+        else:
+            cutoff = float(rmax.cpu().item())
+            peer = host.lsk_peer_choose(box.data_ptr(), all_boxes.data_ptr(), size, cutoff,
+                                        seen.data_ptr(), perm.data_ptr())
+            req = comm.allgather(torch.tensor([peer], dtype=torch.int64, device=comm.device)).view(-1).cpu().tolist()
+            if all(r == -1 for r in req):
+                break
+            sends = [(j, my_tree) for j in range(size) if req[j] == me]
+            recvs = [(peer, (counts[peer], 3), torch.float32)] if peer >= 0 else []
+            got = comm.p2p(sends, recvs)
+            info.timer.mark("peer_exchange")
+            if peer >= 0:
+                seen[peer] = 1
+                work, wn = got[0], counts[peer]
+            else:
+                wn = 0
+        if wn:
+            rmax.zero_()
+            R.run_query(work, wn, points, heaps, cfg.k, cfg.cut2, init=not initialised, rmax=rmax)
+            initialised = True
+        info.timer.mark("knn_rounds")
+    if not initialised:  # empty rank: nothing queried
+        R.run_query(my_tree, 0, points, heaps, cfg.k, cfg.cut2, init=True)
+    out = R.extract(heaps, n, cfg.k)
+    info.timer.mark("return")
+    info.counts["peer_rounds"] = rnd
+    return out

@@ -120,3 +120,75 @@ def test_gloo_two_processes(tmp_path, variant):
         owner = torch.clamp((p[:, 1] * size).long(), max=size - 1)
         for r in range(size):
             assert torch.equal(outs[r], ref[owner == r])
+
+
+# --------------------------------------------------------------------------- ref-algo schedules
+from mpi_cuda_largescaleknn_amd.ops import refalgo as R  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
+
+
+def _check_lbt(tree, n):
+    # left-balanced invariant: left subtree coords <= split <= right subtree coords
+    def sub(t):
+        out, st = [], [t]
+        while st:
+            x = st.pop()
+            if x < n:
+                out.append(x)
+                st += [2 * x + 1, 2 * x + 2]
+        return out
+
+    for t in range(min(n, 200)):
+        level = (t + 1).bit_length() - 1
+        dim = level % 3
+        split = tree[t, dim]
+        for c in sub(2 * t + 1):
+            assert tree[c, dim] <= split
+        for c in sub(2 * t + 2):
+            assert tree[c, dim] >= split
+
+
+def test_lbt_cpu_invariant_and_ids():
+    p = uniform(777, seed=5)
+    tree, ids = R.build_lbt(p)
+    _check_lbt(tree, 777)
+    assert torch.equal(tree, p[ids.long()])
+
+
+@pytest.mark.parametrize("size", [1, 2, 3])
+def test_ring_mode_loopback(size):
+    p = clustered(3000, seed=size)
+    k = 9
+    cfg = E.KnnConfig(k=k)
+
+    def fn(comm):
+        b, e = block(p.shape[0], comm.rank, comm.size)
+        return RA.ring_knn(p[b:e], comm, cfg)
+
+    assert torch.equal(torch.cat(run_loopback(size, fn)), oracle(p, k))
+
+
+@pytest.mark.parametrize("split", ["slab", "random"])
+def test_peer_mode_loopback(split):
+    size = 4
+    p = uniform(4000, seed=12)
+    k = 15
+    if split == "slab":
+        owner = torch.clamp((p[:, 0] * size).long(), max=size - 1)
+    else:
+        owner = torch.randint(0, size, (p.shape[0],), generator=torch.Generator().manual_seed(3))
+    parts = [p[owner == r] for r in range(size)]
+    rounds = {}
+
+    def fn(comm):
+        info = PL.RunInfo(PL.PhaseTimer(False))
+        out = RA.peer_knn(parts[comm.rank], comm, E.KnnConfig(k=k), info)
+        rounds[comm.rank] = info.counts["peer_rounds"]
+        return out
+
+    outs = run_loopback(size, fn)
+    ref = oracle(p, k)
+    for r in range(size):
+        assert torch.equal(outs[r], ref[owner == r])
+    if split == "slab":  # culling: not every rank pulls every shard
+        assert max(rounds.values()) <= size
