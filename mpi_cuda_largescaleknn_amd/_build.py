@@ -59,6 +59,14 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + proc.stdout)
 
 
+# The SLP vectorizer packs the per-candidate distance math into v_pk_* ops, which cannot
+# take the DPP row broadcast as an operand: it adds a v_mov_dpp per operand and ~50 VGPRs.
+FILE_FLAGS = {
+    "knn.hip": ["-fno-slp-vectorize"],
+    "knn_rows.hip": ["-fno-slp-vectorize"],
+}
+
+
 def build_host(force: bool = False, verbose: bool = False) -> str:
     srcs = _sources("host", "cpp")
     if force or _stale(HOST_LIB, srcs + _headers()):
@@ -84,7 +92,7 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     def compile_one(src: str) -> str:
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         if force or _stale(obj, [src] + hdrs):
-            cmd = [hipcc, *HIP_FLAGS, "-c", src, "-o", obj]
+            cmd = [hipcc, *HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             _run(cmd)

@@ -48,6 +48,7 @@ class TreeView(C.Structure):
     _fields_ = [
         ("pts", vp),
         ("nodes", vp),
+        ("qnodes", vp),
         ("n", i64),
         ("depth", C.c_int32),
         ("pad", C.c_int32),
@@ -129,9 +130,10 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_sort_pairs": ([vp, vp, vp, vp, i64, i32, vp, C.POINTER(C.c_int), vp], i32),
         "lsk_hip_tree_depth": ([i64], i32),
         "lsk_hip_tree_nodes": ([i64], i64),
-        "lsk_hip_build_tree": ([vp, i64, vp, vp], i32),
+        "lsk_hip_build_tree": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_tree_set_radii": ([vp, i64, vp, vp], i32),
         "lsk_hip_knn": ([C.POINTER(KnnArgs), vp], i32),
+        "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),
         "lsk_hip_flag_query_groups": ([vp, vp, i64, vp, C.c_int32, i64, vp, vp], i32),
         "lsk_hip_compact_flags": ([vp, i64, vp, vp, vp], i32),
@@ -168,7 +170,10 @@ def hip() -> C.CDLL:
         with _lock:
             if _hip_lib is None:
                 path = _build.HIP_LIB
-                if not os.path.exists(path) or os.environ.get("LSKNN_REBUILD"):
+                override = os.environ.get("LSKNN_HIP_LIB")  # tuning experiments only
+                if override:
+                    path = override
+                elif not os.path.exists(path) or os.environ.get("LSKNN_REBUILD"):
                     path = _build.build_hip()
                 else:
                     # rebuild if sources changed (cheap mtime check; needs hipcc)

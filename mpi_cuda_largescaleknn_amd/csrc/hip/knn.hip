@@ -429,6 +429,11 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
   const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
   s.cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
   s.band_lo = s.band_w = s.m = s.bc = s.coff = s.ccnt = 0;
+  // every lane's histogram state is defined (lanes that never histogram included:
+  // the wave-wide shrink step reads bin_hi / c_hi of all lanes)
+  s.lo_b = s.hi_b = s.shift = s.c_hi = 0;
+  s.bin_hi = 0;
+  s.zc = 0;
   s.ans = cut_b;
 
   int64_t total_pts = 0;
@@ -466,7 +471,11 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
         break;
       }
       hist_passes++;
-      if (s.state != ST_HIST) s.hi_b = 0;
+      if (s.state != ST_HIST) {  // not histogramming this pass: count nothing
+        s.hi_b = 0;
+        s.c_hi = 0;
+        s.bin_hi = 0;
+      }
 #pragma unroll 8
       for (int j = 0; j < kPool / lsk::kWave; j++) W.L->pool[j * lsk::kWave + lane] = 0u;
       if (first || !W.list_ok) traverse<MODE_HIST>(s, W, A, first);

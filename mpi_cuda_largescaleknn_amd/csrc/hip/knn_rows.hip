@@ -1,0 +1,793 @@
+// k-th-NN distance selection, row-decomposed variant (the production kernel).
+//
+// Same contract and selection algorithm as knn.hip (two-pass radix select on d² bits
+// with a per-lane LDS histogram, LDS collect pool and per-lane (k-c_lo)-max-heap; see the
+// header of knn.hip and the reference runQuery/extractFinalResult,
+// unorderedDataVariant.cu:75-103), with a different SIMD decomposition:
+//
+//  * a wave owns 64 consecutive Morton-sorted queries split into 4 ROWS of 16 (the
+//    16-lane rows of CDNA4 DPP). The tree walk is still wave-uniform (LDS stack, scalar
+//    node loads), but at a 64-point leaf each row tests the leaf's four 16-point QUARTER
+//    boxes with its own 16 lanes and appends the quarters it needs to its own LDS list;
+//  * rows consume their lists in lockstep: one step = one quarter per row, the 16
+//    candidates of each row's quarter are loaded by the row's 16 lanes (one vector load,
+//    prefetched one step ahead) and broadcast inside the row with DPP row_newbcast, which
+//    the compiler folds into v_subrev_f32_dpp — the broadcast costs nothing;
+//  * so a query evaluates only candidates of quarters its own 16-query row needs (small
+//    union of balls, 16-point culling granularity) instead of everything its 64-query
+//    group needs.
+//  * the walk and the processing alternate (fill the row lists until every row has a
+//    batch pending, then drain in lockstep), so each list is a short work queue. With a
+//    large capacity (RCAP=256) the lists recorded in pass 1 are also replayed (filtered +
+//    compacted per row) by the retry and collect passes, but the LDS that costs lowers
+//    occupancy by more than the replay saves; the default RCAP=32 re-walks each pass.
+//  * histogram bin index = sat(d²bits - lo) >> shift: values below the range land in bin
+//    0 (no separate compare), and c_base tracks how many of them are known to be below.
+//  Inner-loop cost per candidate and lane: 6 VALU for d² (DPP broadcast folded into the
+//  subtracts) + 8 VALU + 1 ds_add for the histogram (compiled with -fno-slp-vectorize:
+//  packed-math ops cannot take DPP operands).
+#include "dev.h"
+
+namespace {
+
+using lsk::bitsf;
+using lsk::fbits;
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kThreads = kWavesPerBlock * lsk::kWave;
+#ifndef LSK_ROWS_BINS
+#define LSK_ROWS_BINS 64
+#endif
+#ifndef LSK_ROWS_MINW
+#define LSK_ROWS_MINW 1
+#endif
+constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
+static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
+constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
+constexpr int kStackCap = 64;
+constexpr uint32_t kShift0 = 20;
+constexpr uint32_t kMaxPasses = 96;
+constexpr uint32_t kGuardRounds = 1u << 22;
+constexpr uint32_t kInvalid = 0xffffffffu;
+constexpr uint32_t kUnknown = 0xffffffffu;
+
+enum : uint32_t { ST_HIST = 0, ST_READY = 1, ST_DONE = 2 };
+enum { MODE_HIST = 0, MODE_COLLECT = 1 };
+
+struct WaveLds {
+  uint32_t pool[kPool];
+  uint32_t stack[kStackCap];
+};
+// + per-row quarter lists (RCAP entries per row), a kernel template parameter: it sets
+// the LDS footprint and so the occupancy
+template <int RCAP>
+struct WaveLdsR {
+  WaveLds w;
+  uint32_t rl[4 * RCAP];
+};
+
+struct Lane {
+  float qx, qy, qz;
+  uint32_t state;
+  uint32_t lo_b, hi_b, shift;
+  int32_t bin_hi;
+  uint32_t c_hi;
+  uint32_t c_base;  // exact count of values < lo_b, or kUnknown
+  uint32_t nudf;    // underflow retries so far
+  uint32_t cut_lim;
+  uint32_t band_lo, band_w, m, bc;
+  uint32_t coff, ccnt;
+  uint32_t ans;
+};
+
+// Histogram range [lo_b, hi_b) in 64 bins of 2^shift float bits. Values below lo_b are
+// counted in bin 0 (saturating bin index), so bin 0 is [0, lo_b + 2^shift); c_base is
+// the exact number of values below lo_b when a previous pass established it.
+__device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift, uint32_t top_limit,
+                                          uint32_t c_base) {
+  s.lo_b = lo_b;
+  s.c_base = lo_b == 0 ? 0u : c_base;
+  s.shift = shift;
+  uint64_t top = (uint64_t)lo_b + ((uint64_t)kBins << shift);
+  uint64_t hi = top < (uint64_t)top_limit ? top : (uint64_t)top_limit;
+  s.hi_b = (uint32_t)hi;
+  s.bin_hi = hi > lo_b ? (int32_t)((hi - lo_b + ((1ull << shift) - 1)) >> shift) : 0;
+  s.c_hi = 0;
+}
+
+__device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
+  return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
+}
+
+__device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *pool, int lane) {
+  return s.bin_hi > 0 ? hist_read(pool, (uint32_t)s.bin_hi - 1u, lane) : s.c_hi;
+}
+
+__device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
+  while (s.bin_hi > 0) {
+    const uint32_t top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
+    if (s.c_hi - top < k) break;
+    s.c_hi -= top;
+    s.bin_hi--;
+    s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
+  }
+}
+
+// DPP row_newbcast:J — lane J of each 16-lane row to the whole row (folded into the
+// consuming VALU op as a DPP source).
+template <int J>
+__device__ __forceinline__ float rowb(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + J, 0xf, 0xf, false));
+}
+
+// Candidate J of the row's quarter (padding lanes hold +inf coordinates: d² = inf,
+// which is above every histogram range and collect band).
+template <int J>
+__device__ __forceinline__ uint32_t cand(const Lane &s, float px, float py, float pz) {
+  const float d2 = lsk::dist2(s.qx - rowb<J>(px), s.qy - rowb<J>(py), s.qz - rowb<J>(pz));
+  return fbits(d2);
+}
+
+template <int MODE>
+__device__ __forceinline__ void update8(Lane &s, const uint32_t (&u)[8], uint32_t *pool, int lane) {
+  uint32_t umin = u[0];
+#pragma unroll
+  for (int t = 1; t < 8; t++) umin = min(umin, u[t]);
+  if (MODE == MODE_HIST) {
+    if (!__ballot(umin < s.hi_b)) return;
+    // bin = sat(v - lo_b) >> shift (< 64 for every v < hi_b); bins 2j, 2j+1 share the
+    // lane's dword j as two 16-bit counters
+    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const uint32_t v = u[t];
+      const bool in = v < hb;
+      const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
+      uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
+      if (kBins < 64) dw = min(dw, (uint32_t)(kBins / 2 - 1));  // stay inside the pool
+      const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
+      const uint32_t inc = in ? __umul24(half, 0xffffu) + 1u : 0u;
+      atomicAdd(&pool[dw * lsk::kWave + lane], inc);
+      s.c_hi += (uint32_t)in;
+    }
+  } else {
+    const uint32_t bl = s.band_lo, bw = s.band_w;
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < 8; t++) any = any || (u[t] - bl < bw);
+    if (!__ballot(any)) return;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      if (u[t] - bl < bw) {
+        if (s.ccnt < s.bc) pool[s.coff + s.ccnt] = u[t];
+        s.ccnt++;
+      }
+    }
+  }
+}
+
+// The 16 candidates of this lane's row quarter (lane i of the row holds candidate i).
+template <int MODE>
+__device__ __forceinline__ void process16(Lane &s, float px, float py, float pz, uint32_t cnt,
+                                          uint32_t *pool, int lane, uint32_t k) {
+  {
+    uint32_t u[8] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
+                     cand<3>(s, px, py, pz), cand<4>(s, px, py, pz), cand<5>(s, px, py, pz),
+                     cand<6>(s, px, py, pz), cand<7>(s, px, py, pz)};
+    update8<MODE>(s, u, pool, lane);
+  }
+  if (__ballot(cnt > 8u)) {
+    uint32_t u[8] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
+                     cand<11>(s, px, py, pz), cand<12>(s, px, py, pz), cand<13>(s, px, py, pz),
+                     cand<14>(s, px, py, pz), cand<15>(s, px, py, pz)};
+    update8<MODE>(s, u, pool, lane);
+  }
+  if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) hist_shrink(s, pool, lane, k);
+}
+
+struct WaveCtx {
+  WaveLds *L;
+  uint32_t *rl;
+  uint32_t rcap;
+  int lane, row;
+  uint32_t k;
+  uint32_t g;
+  int32_t seed;
+  float cx, cy, cz;
+  uint32_t len0, len1, len2, len3;  // row list lengths (wave-uniform)
+  uint32_t done;                    // lockstep steps already processed
+  bool list_ok;
+  uint32_t guard;  // watchdog trips of the walk (never expected; see traverse)
+  uint32_t steps, quarters, nodes_visited, csteps, cnodes;
+};
+
+__device__ __forceinline__ uint32_t row_len(const WaveCtx &W, int row) {
+  return row == 0 ? W.len0 : row == 1 ? W.len1 : row == 2 ? W.len2 : W.len3;
+}
+__device__ __forceinline__ uint32_t max_len(const WaveCtx &W) {
+  return max(max(W.len0, W.len1), max(W.len2, W.len3));
+}
+__device__ __forceinline__ uint32_t min_len(const WaveCtx &W) {
+  return min(min(W.len0, W.len1), min(W.len2, W.len3));
+}
+
+__device__ __forceinline__ lsk_tree_view pick_tree(const lsk_knn_args &A, uint32_t t) {
+  return t ? A.tree[1] : A.tree[0];
+}
+
+// Entry = (tree << 31) | quarter id. Loads this lane's candidate of its row's quarter.
+// Branch-free (the load is always issued, from a clamped in-bounds address), so the
+// compiler can count outstanding loads and the prefetch is not serialised by vmcnt(0).
+__device__ __forceinline__ uint32_t load_quarter(const lsk_knn_args &A, uint32_t e, int lane,
+                                                 float &px, float &py, float &pz) {
+  const bool ok = e != kInvalid;
+  // invalid entries read point 0 of a non-empty tree (lists only exist when one is)
+  const bool t1 = ok ? (e >> 31) != 0 : A.tree[0].n <= 0;
+  const float *pts = t1 ? A.tree[1].pts : A.tree[0].pts;
+  const int64_t n = t1 ? A.tree[1].n : A.tree[0].n;
+  const int64_t base = ok ? (int64_t)(e & 0x7fffffffu) * 16 : 0;
+  const int64_t rem = ok ? n - base : 0;
+  const int64_t j = (int64_t)(lane & 15);
+  const bool live = j < rem;
+  const float *p = pts + 3 * (live ? base + j : 0);
+  px = p[0];  // raw: the consumer substitutes +inf for padding lanes (see process_steps)
+  py = p[1];
+  pz = p[2];
+  return rem < 16 ? (uint32_t)rem : 16u;
+}
+
+__device__ __forceinline__ uint32_t row_entry(const WaveCtx &W, uint32_t step) {
+  const uint32_t v = W.rl[(uint32_t)W.row * W.rcap + min(step, W.rcap - 1u)];
+  return step < row_len(W, W.row) ? v : kInvalid;
+}
+
+// Lockstep processing of steps [b, e): row r handles its list entry `step`.
+template <int MODE>
+__device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn_args &A,
+                                              uint32_t b, uint32_t e) {
+  b = lsk::uniform(b);  // wave-uniform loop (lets the compiler keep it scalar)
+  e = lsk::uniform(e);
+  if (b >= e) return;
+  // one step of prefetch; loads are unconditional (clamped step) so no branch breaks
+  // the compiler's count of outstanding loads
+  const uint32_t last = e - 1;
+  float px, py, pz;
+  uint32_t cnt = load_quarter(A, row_entry(W, b), W.lane, px, py, pz);
+  const float inf = __builtin_inff();
+  for (uint32_t st = b; st < e; st++) {
+    const uint32_t ccnt = cnt;
+    const bool live = (uint32_t)(W.lane & 15) < ccnt;
+    const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
+    cnt = load_quarter(A, row_entry(W, min(st + 1, last)), W.lane, px, py, pz);
+    W.steps++;
+    if (MODE == MODE_COLLECT) W.csteps++;
+    process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+  }
+}
+
+__device__ __forceinline__ float hist_bound(const Lane &s) { return bitsf(s.hi_b); }
+
+// per-lane need of a box in a given mode. HIST: closer than the lane's radius; COLLECT:
+// box cuts the lane's shell [band_lo, band_hi) (max-distance is monotone, common.h).
+template <int MODE>
+__device__ __forceinline__ bool box_needed(const Lane &s, float lx, float ly, float lz, float hx,
+                                           float hy, float hz) {
+  const lsk::vec3f q{s.qx, s.qy, s.qz};
+  if (MODE == MODE_HIST) return lsk::box_dist2(q, {lx, ly, lz}, {hx, hy, hz}) < hist_bound(s);
+  if (s.band_w == 0) return false;
+  const bool near = lsk::box_dist2(q, {lx, ly, lz}, {hx, hy, hz}) < bitsf(s.band_lo + s.band_w);
+  const float fx = fmaxf(fabsf(lx - s.qx), fabsf(hx - s.qx));
+  const float fy = fmaxf(fabsf(ly - s.qy), fabsf(hy - s.qy));
+  const float fz = fmaxf(fabsf(lz - s.qz), fabsf(hz - s.qz));
+  return near && fbits(lsk::dist2(fx, fy, fz)) >= s.band_lo;
+}
+
+// Box kept by a replay filter: any future use (HIST lanes: radius, READY lanes: shell).
+template <int MODE>
+__device__ __forceinline__ bool box_retained(const Lane &s, float lx, float ly, float lz, float hx,
+                                             float hy, float hz) {
+  if (MODE == MODE_COLLECT) return box_needed<MODE_COLLECT>(s, lx, ly, lz, hx, hy, hz);
+  if (s.state == ST_HIST) return box_needed<MODE_HIST>(s, lx, ly, lz, hx, hy, hz);
+  if (s.state == ST_READY) return box_needed<MODE_COLLECT>(s, lx, ly, lz, hx, hy, hz);
+  return false;
+}
+
+__device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
+  return ((ballot & 0xffffull) ? 1u : 0u) | ((ballot & 0xffff0000ull) ? 2u : 0u) |
+         ((ballot & 0xffff00000000ull) ? 4u : 0u) | ((ballot & 0xffff000000000000ull) ? 8u : 0u);
+}
+
+__device__ __forceinline__ void rows_append(WaveCtx &W, uint32_t rowmask, uint32_t e) {
+  if (rowmask & 1u) { if (W.lane == 0) W.rl[0u * W.rcap + W.len0] = e; W.len0++; }
+  if (rowmask & 2u) { if (W.lane == 0) W.rl[1u * W.rcap + W.len1] = e; W.len1++; }
+  if (rowmask & 4u) { if (W.lane == 0) W.rl[2u * W.rcap + W.len2] = e; W.len2++; }
+  if (rowmask & 8u) { if (W.lane == 0) W.rl[3u * W.rcap + W.len3] = e; W.len3++; }
+  W.quarters += __popc(rowmask);
+}
+
+// Tree walk (wave-uniform DFS, near child first) building the per-row quarter lists,
+// alternating with lockstep processing of what every row has pending (one processing
+// call site per pass keeps the kernel's register allocation tight). Seeding: tree 0's
+// buckets [g-seed, g+seed] are queued for every row first and skipped by the walk.
+// A list that would overflow forces a drain and a reset (replay then disabled).
+template <int MODE>
+__device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
+  const lsk::vec3f q{s.qx, s.qy, s.qz};
+  const lsk::vec3f c{W.cx, W.cy, W.cz};
+  W.len0 = W.len1 = W.len2 = W.len3 = 0;
+  W.done = 0;
+  uint32_t t = 0, sp = 0;
+  bool started = false, finished = false;
+  int32_t seed_d = W.seed > 0 ? 0 : -1;  // next seed distance (tree 0 only)
+  lsk_tree_view T = pick_tree(A, 0);
+  uint32_t leaf0 = 0, nquarters = 0, nbuckets = 0;
+  int64_t skip_lo = 1, skip_hi = 0;
+  uint32_t fill_rounds = 0;
+  while (!finished) {
+    bool overflow = false;
+    if (++fill_rounds > kGuardRounds) {  // watchdog: never spin on the GPU
+      W.guard |= 1u;
+      break;
+    }
+    // ---- fill until every row has a batch pending, a list is nearly full or the walk ends
+    for (;;) {
+      if (max_len(W) + 4u > W.rcap) {
+        overflow = true;
+        break;
+      }
+      if (min_len(W) >= W.done + 8u) break;
+      if (!started) {
+        if (t >= (uint32_t)A.ntrees) {
+          finished = true;
+          break;
+        }
+        T = pick_tree(A, t);
+        if (T.n <= 0) {
+          t++;
+          continue;
+        }
+        leaf0 = 1u << T.depth;
+        nquarters = (uint32_t)((T.n + 15) / 16);
+        nbuckets = (uint32_t)((T.n + lsk::kBucket - 1) / lsk::kBucket);
+        skip_lo = 1;
+        skip_hi = 0;
+        if (t == 0 && W.seed > 0) {
+          skip_lo = (int64_t)W.g - W.seed;
+          skip_hi = (int64_t)W.g + W.seed;
+        }
+        if (W.lane == 0) W.L->stack[0] = 1u;
+        sp = 1;
+        started = true;
+      }
+      if (t == 0 && seed_d >= 0) {  // seed buckets g, g-1, g+1, g-2, g+2, ... for every row
+        for (int32_t sgn = 0; sgn < (seed_d ? 2 : 1); sgn++) {
+          const int64_t b = sgn ? (int64_t)W.g + seed_d : (int64_t)W.g - seed_d;
+          if (b < 0 || b >= (int64_t)nbuckets) continue;
+          for (uint32_t qq = 0; qq < 4; qq++) {
+            const uint32_t qid = (uint32_t)b * 4 + qq;
+            if (qid < nquarters) rows_append(W, 0xfu, qid);
+          }
+        }
+        seed_d = seed_d < W.seed ? seed_d + 1 : -1;
+        continue;
+      }
+      if (sp == 0) {
+        t++;
+        started = false;
+        continue;
+      }
+      lsk::cfloat4_p nodes = lsk::as_const4(T.nodes);
+      sp--;
+      const uint32_t node = lsk::uniform(W.L->stack[sp]);
+      W.nodes_visited++;
+      if (MODE == MODE_COLLECT) W.cnodes++;
+      if (node >= leaf0) {
+        const uint32_t b = node - leaf0;
+        if (b >= nbuckets || ((int64_t)b >= skip_lo && (int64_t)b <= skip_hi)) continue;
+        lsk::cfloat4_p qnodes = lsk::as_const4(T.qnodes);
+#pragma unroll
+        for (uint32_t qq = 0; qq < 4; qq++) {
+          const uint32_t qid = b * 4 + qq;
+          if (qid >= nquarters) break;
+          const lsk::v4f lo = qnodes[2 * qid], hi = qnodes[2 * qid + 1];
+          const uint64_t m = __ballot(box_needed<MODE>(s, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z));
+          rows_append(W, row_bits(m), (t << 31) | qid);
+        }
+        continue;
+      }
+      const float lim = MODE == MODE_HIST ? hist_bound(s)
+                                          : (s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f);
+      const lsk::v4f lo = nodes[2 * node], hi = nodes[2 * node + 1];
+      if (!__ballot(lsk::box_dist2(q, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}) < lim)) continue;
+      const uint32_t c0 = 2 * node, c1 = c0 + 1;
+      const lsk::v4f l0 = nodes[2 * c0], h0 = nodes[2 * c0 + 1];
+      const lsk::v4f l1 = nodes[2 * c1], h1 = nodes[2 * c1 + 1];
+      const bool n0 = __ballot(lsk::box_dist2(q, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z}) < lim) != 0;
+      const bool n1 = __ballot(lsk::box_dist2(q, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z}) < lim) != 0;
+      const float g0 = lsk::box_dist2(c, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z});
+      const float g1 = lsk::box_dist2(c, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z});
+      const bool first0 = g0 <= g1;
+      const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
+      const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
+      if (na) {
+        if (W.lane == 0) W.L->stack[sp] = a;
+        sp++;
+      }
+      if (nbb) {
+        if (W.lane == 0) W.L->stack[sp] = bb;
+        sp++;
+      }
+    }
+    // ---- drain (single processing call site)
+    const uint32_t target = (finished || overflow) ? max_len(W) : min_len(W);
+    process_steps<MODE>(s, W, A, W.done, target);
+    W.done = target;
+    if (overflow) {
+      W.len0 = W.len1 = W.len2 = W.len3 = 0;
+      W.done = 0;
+      W.list_ok = false;
+    }
+  }
+}
+
+// Filter + compact every row's recorded list (in place, lockstep), then process it.
+template <int MODE>
+__device__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
+  const uint32_t total = max_len(W);
+  uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+  for (uint32_t st = 0; st < total; st++) {
+    const uint32_t e = row_entry(W, st);
+    bool keep = false;
+    if (e != kInvalid) {
+      const float *qn = (e >> 31) ? A.tree[1].qnodes : A.tree[0].qnodes;  // per-lane select
+      const float4 *qb = (const float4 *)qn + 2 * (size_t)(e & 0x7fffffffu);
+      const float4 lo = qb[0], hi = qb[1];
+      keep = box_retained<MODE>(s, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+    }
+    const uint32_t rb = row_bits(__ballot(keep));
+    // lane 16r holds row r's entry
+    if ((W.lane & 15) == 0) {
+      const uint32_t r = (uint32_t)W.row;
+      const uint32_t pos = r == 0 ? n0 : r == 1 ? n1 : r == 2 ? n2 : n3;
+      if ((rb >> r) & 1u) W.rl[r * W.rcap + pos] = e;
+    }
+    n0 += rb & 1u;
+    n1 += (rb >> 1) & 1u;
+    n2 += (rb >> 2) & 1u;
+    n3 += (rb >> 3) & 1u;
+  }
+  W.len0 = n0;
+  W.len1 = n1;
+  W.len2 = n2;
+  W.len3 = n3;
+  W.done = 0;
+  process_steps<MODE>(s, W, A, 0, max_len(W));
+  W.done = max_len(W);
+}
+
+__device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
+  const uint32_t v = h[i];
+  for (;;) {
+    uint32_t l = 2 * i + 1, r = l + 1, c = i;
+    uint32_t cv = v;
+    if (l < m && h[l] > cv) { c = l; cv = h[l]; }
+    if (r < m && h[r] > cv) { c = r; cv = h[r]; }
+    if (c == i) break;
+    h[i] = cv;
+    i = c;
+  }
+  h[i] = v;
+}
+
+__device__ __forceinline__ float bcast64(float v, uint32_t j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
+}
+
+__device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k) {
+  constexpr int M = 8;
+  float best[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) best[i] = __builtin_inff();
+  for (uint32_t j0 = 0; j0 < nvalid; j0 += 8) {
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const uint32_t j = j0 + (uint32_t)t;
+      float v = lsk::dist2(s.qx - bcast64(s.qx, j), s.qy - bcast64(s.qy, j), s.qz - bcast64(s.qz, j));
+      v = (j < nvalid) ? v : __builtin_inff();
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const float lo = fminf(best[i], v);
+        v = fmaxf(best[i], v);
+        best[i] = lo;
+      }
+    }
+  }
+  const uint32_t m0 = k < (uint32_t)M ? k : (uint32_t)M;
+  float dm = best[0];
+#pragma unroll
+  for (int i = 1; i < M; i++) dm = (i + 1 == (int)m0) ? best[i] : dm;
+  return dm * cbrtf(((float)k / (float)m0) * ((float)k / (float)m0));
+}
+
+enum : uint32_t {
+  QS_OVERFLOW = 1, QS_UNDERFLOW = 2, QS_REFINE = 4, QS_LIST_INVALID = 8, QS_COLLECTED = 16,
+  QS_DONE_BAND1 = 32, QS_DONE_CUT = 64, QS_DONE_ZERO = 128, QS_LIMIT = 256, QS_MISMATCH = 512,
+  QS_HINT = 1024
+};
+
+template <int RCAP>
+__global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const lsk_knn_args A) {
+  __shared__ WaveLdsR<RCAP> lds[kWavesPerBlock];
+  const int wid = threadIdx.x >> 6;
+  const int lane = lsk::lane_id();
+  const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
+  const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid;
+  const uint64_t ngroups = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+  if (wave >= ngroups) return;
+  const uint32_t g = lsk::uniform(A.groups ? A.groups[wave] : (uint32_t)wave);
+  const int64_t q0 = (int64_t)g * lsk::kBucket;
+  const int64_t qi = q0 + lane;
+  const bool valid = qi < A.nq;
+  const uint32_t nvalid = (uint32_t)((A.nq - q0) < lsk::kBucket ? (A.nq - q0) : lsk::kBucket);
+  const uint32_t k = (uint32_t)A.k;
+
+  WaveCtx W;
+  W.L = &lds[wid].w;
+  W.rl = lds[wid].rl;
+  W.rcap = RCAP;
+  W.lane = lane;
+  W.row = lane >> 4;
+  W.k = k;
+  W.g = g;
+  W.seed = A.seed;
+  W.len0 = W.len1 = W.len2 = W.len3 = 0;
+  W.done = 0;
+  W.list_ok = true;
+  W.guard = 0;
+  W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
+
+  Lane s;
+  s.qx = valid ? A.qpts[3 * qi] : 0.f;
+  s.qy = valid ? A.qpts[3 * qi + 1] : 0.f;
+  s.qz = valid ? A.qpts[3 * qi + 2] : 0.f;
+  uint32_t qs = 0;
+
+  const float inf = __builtin_inff();
+  const float lx = lsk::wave_min(valid ? s.qx : inf), hx = lsk::wave_max(valid ? s.qx : -inf);
+  const float ly = lsk::wave_min(valid ? s.qy : inf), hy = lsk::wave_max(valid ? s.qy : -inf);
+  const float lz = lsk::wave_min(valid ? s.qz : inf), hz = lsk::wave_max(valid ? s.qz : -inf);
+  W.cx = 0.5f * (lx + hx);
+  W.cy = 0.5f * (ly + hy);
+  W.cz = 0.5f * (lz + hz);
+
+  float r_est2 = own_group_estimate(s, nvalid, k);
+  if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
+    r_est2 = A.r_hint2;
+    qs |= QS_HINT;
+  }
+  if (!(r_est2 > 0.f) || !(r_est2 < inf)) r_est2 = 1.f;
+
+  const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
+  s.cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
+  s.band_lo = s.band_w = s.m = s.bc = s.coff = s.ccnt = 0;
+  // every lane's histogram state is defined (lanes that never histogram included:
+  // the wave-wide shrink step reads bin_hi / c_hi of all lanes)
+  s.lo_b = s.hi_b = s.shift = s.c_hi = 0;
+  s.bin_hi = 0;
+  s.c_base = 0;
+  s.nudf = 0;
+  s.ans = cut_b;
+
+  int64_t total_pts = 0;
+  for (int t = 0; t < A.ntrees; t++) total_pts += pick_tree(A, t).n;
+
+  uint32_t hist_passes = 0, limit = 0;
+  if (!valid || total_pts < (int64_t)k) {
+    s.state = ST_DONE;
+    s.hi_b = 0;
+    qs |= QS_DONE_CUT;
+  } else {
+    s.state = ST_HIST;
+    const uint32_t est_b = fbits(r_est2);
+    const uint32_t off = (uint32_t)(kBins - 16) << kShift0;  // range top 2 octaves above
+    const uint32_t lo0 = est_b > off ? est_b - off : 0u;
+    set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
+  }
+
+  uint32_t pool_off = 0;
+  bool first = true;
+  uint32_t passes = 0;
+  // terminates: every round runs >= 1 pass (a round that does not break refines at
+  // least one lane: total > kPool implies some lane has bc > kPool / 64), and the
+  // passes are capped at kMaxPasses
+  for (;;) {
+    while (__ballot(s.state == ST_HIST)) {
+      if (++passes > kMaxPasses) {
+        limit = 1;
+        if (s.state == ST_HIST) {
+          s.state = ST_DONE;
+          s.ans = 0x7fc00000u;
+          qs |= QS_LIMIT;
+        }
+        break;
+      }
+      hist_passes++;
+      if (s.state != ST_HIST) {  // not histogramming this pass: count nothing
+        s.hi_b = 0;
+        s.c_hi = 0;
+        s.bin_hi = 0;
+      }
+#pragma unroll 8
+      for (int j = 0; j < kPool / lsk::kWave; j++) W.L->pool[j * lsk::kWave + lane] = 0u;
+      if (first || !W.list_ok) {
+        if (!first) W.list_ok = false;  // lists rebuilt as work queues only
+        traverse<MODE_HIST>(s, W, A);
+        if (!first) W.list_ok = false;
+      } else {
+        replay<MODE_HIST>(s, W, A);
+      }
+      first = false;
+      bool ovf = false;
+      if (s.state == ST_HIST) {
+        const uint32_t top = top_count(s, W.L->pool, lane);
+        if (s.c_hi < k) {
+          if (s.hi_b >= s.cut_lim) {
+            s.state = ST_DONE;
+            s.ans = cut_b;
+            qs |= QS_DONE_CUT;
+          } else {
+            ovf = true;
+            qs |= QS_OVERFLOW;
+            set_range(s, s.hi_b, kShift0, s.cut_lim, s.c_hi);
+          }
+        } else if (s.bin_hi <= 1 && s.c_base == kUnknown) {
+          // k-th in bin 0, which also holds every value below lo_b: the estimate was
+          // too large. First time: the 8 octaves below. Again: everything below, in 64
+          // coarse bins (then refined) — also how a k-th distance of 0 is reached.
+          qs |= QS_UNDERFLOW;
+          const uint32_t topb = s.hi_b;  // = lo_b + 2^shift, or the clipped top
+          if (s.nudf == 0 && topb > ((uint32_t)kBins << kShift0)) {
+            set_range(s, topb - ((uint32_t)kBins << kShift0), kShift0, topb, kUnknown);
+          } else {
+            uint32_t sh = 0;
+            while (((uint64_t)kBins << sh) < (uint64_t)topb) sh++;
+            set_range(s, 0u, sh, topb, 0u);
+          }
+          s.nudf++;
+        } else {
+          // band = bin bin_hi-1; bin 0 loses its saturated part (c_base values < lo_b)
+          const uint32_t below = s.bin_hi == 1 ? s.c_base : s.c_hi - top;
+          const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
+          const uint32_t bw = s.hi_b - bl;
+          if (bw <= 1u) {
+            s.state = ST_DONE;
+            s.ans = bl;
+            qs |= QS_DONE_BAND1;
+          } else {
+            s.state = ST_READY;
+            s.band_lo = bl;
+            s.band_w = bw;
+            s.m = k - below;
+            s.bc = s.c_hi - below;
+          }
+        }
+      }
+      if (__ballot(ovf)) W.list_ok = false;
+    }
+    if (limit) break;
+    const uint32_t need = s.state == ST_READY ? s.bc : 0u;
+    uint32_t x = need;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    const uint32_t total = __shfl(x, 63);
+    pool_off = x - need;
+    if (total <= (uint32_t)kPool) break;
+    if (s.state == ST_READY && s.bc > (uint32_t)(kPool / lsk::kWave)) {
+      qs |= QS_REFINE;
+      const uint32_t sh = s.shift >= 6u ? s.shift - 6u : 0u;
+      set_range(s, s.band_lo, sh, s.band_lo + s.band_w, k - s.m);
+      s.band_lo = s.band_w = 0;
+      s.state = ST_HIST;
+    }
+  }
+
+  if (!W.list_ok) qs |= QS_LIST_INVALID;
+  if (!limit && __ballot(s.state == ST_READY)) {
+    if (s.state != ST_READY) s.band_lo = s.band_w = 0;
+    s.coff = pool_off;
+    s.ccnt = 0;
+    if (W.list_ok) replay<MODE_COLLECT>(s, W, A);
+    else traverse<MODE_COLLECT>(s, W, A);
+    if (s.state == ST_READY) {
+      qs |= QS_COLLECTED;
+      if (s.ccnt != s.bc) qs |= QS_MISMATCH;
+      uint32_t *h = W.L->pool + s.coff;
+      const uint32_t c = min(s.ccnt, s.bc), m = s.m;
+      if (m >= 1 && m <= c) {
+        for (int i = (int)(m / 2) - 1; i >= 0; i--) heap_sift(h, (uint32_t)i, m);
+        for (uint32_t i = m; i < c; i++) {
+          const uint32_t v = h[i];
+          if (v < h[0]) {
+            h[0] = v;
+            heap_sift(h, 0, m);
+          }
+        }
+        s.ans = h[0];
+      } else {
+        qs |= QS_MISMATCH;
+        s.ans = 0x7fc00000u;
+      }
+    }
+  }
+
+  if (valid) {
+    A.out_d2[qi] = bitsf(s.ans);
+    if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
+  }
+
+  if (A.stats) {
+    auto cnt = [&](uint32_t bit) {
+      return (unsigned long long)__popcll(__ballot(valid && (qs & bit)));
+    };
+    const unsigned long long c_ovf = cnt(QS_OVERFLOW), c_udf = cnt(QS_UNDERFLOW),
+                             c_ref = cnt(QS_REFINE), c_mm = cnt(QS_MISMATCH), c_hint = cnt(QS_HINT);
+    if (lane == 0) {
+      atomicAdd(&A.stats[0], (unsigned long long)W.steps * 16ull);  // candidates per lane
+      atomicAdd(&A.stats[1], (unsigned long long)W.quarters);
+      atomicAdd(&A.stats[2], (unsigned long long)W.nodes_visited);
+      atomicAdd(&A.stats[3], (unsigned long long)hist_passes);
+      atomicAdd(&A.stats[4], c_ovf);
+      atomicAdd(&A.stats[5], c_udf);
+      atomicAdd(&A.stats[6], c_ref);
+      atomicAdd(&A.stats[7], c_mm);
+      atomicAdd(&A.stats[8], (unsigned long long)limit);
+      atomicAdd(&A.stats[9], W.list_ok ? 0ull : 1ull);
+      atomicAdd(&A.stats[10], 1ull);
+      atomicAdd(&A.stats[11], c_hint);
+      atomicAdd(&A.stats[12], (unsigned long long)W.steps);
+      atomicAdd(&A.stats[13], (unsigned long long)W.csteps);
+      atomicAdd(&A.stats[14], (unsigned long long)W.cnodes);
+      atomicAdd(&A.stats[15], (unsigned long long)W.guard);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
+  const lsk_knn_args &A = *args;
+  if (A.k < 1 || A.k > 65535) {
+    lsk::set_last_error("knn_rows: k must be in [1, 65535] for the radix-select kernel");
+    return 1;
+  }
+  if (A.nq >= ((int64_t)1 << 32) || A.ntrees < 0 || A.ntrees > 2 || A.seed < 0 || A.seed > 64) {
+    lsk::set_last_error("knn_rows: nq must be < 2^32, ntrees in [0,2], seed in [0,64]");
+    return 1;
+  }
+  for (int t = 0; t < A.ntrees; t++) {
+    if (A.tree[t].n >= ((int64_t)1 << 31) || A.tree[t].depth > 26 || !A.tree[t].qnodes) {
+      lsk::set_last_error("knn_rows: tree too large or quarter boxes missing");
+      return 1;
+    }
+  }
+  const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
+  if (ngroups <= 0) return 0;
+  const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
+  // Row-list capacity: 32 entries keeps the block at 35 KB of LDS (4 waves/SIMD) and
+  // uses the lists only as per-pass work queues; 256 also replays them across passes but
+  // costs one wave/SIMD of occupancy (measured slower: 0.52 vs 0.46 s, 1e8 pts, k=100).
+  // LSK_ROWS_RCAP=256 selects the replaying variant (tuning experiments).
+  static const int rcap = [] {
+    const char *e = getenv("LSK_ROWS_RCAP");
+    return e ? atoi(e) : 32;
+  }();
+  if (rcap == 256)
+    knn_rows_kernel<256><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+  else
+    knn_rows_kernel<32><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+  LSK_CHECK_LAUNCH("knn_rows");
+  return 0;
+}

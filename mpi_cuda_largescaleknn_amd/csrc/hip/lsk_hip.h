@@ -62,7 +62,10 @@ int lsk_hip_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint3
 // ---- bucket tree ---------------------------------------------------------------------
 int lsk_hip_tree_depth(int64_t n);          // depth for 64-point buckets
 int64_t lsk_hip_tree_nodes(int64_t n);      // number of node slots (2^(depth+1))
-int lsk_hip_build_tree(const float *sorted_pts, int64_t n, float *nodes, void *stream);
+// qnodes (optional, 2^depth*4 x 2 float4): boxes of the four 16-point quarters of
+// every bucket (quarter q of bucket b = sorted points [64b+16q, 64b+16q+16)).
+int lsk_hip_build_tree(const float *sorted_pts, int64_t n, float *nodes, float *qnodes,
+                       void *stream);
 // leaves' lo.w = max over the bucket's queries of d2[i]; propagated to all levels.
 int lsk_hip_tree_set_radii(float *nodes, int64_t n, const float *d2_sorted, void *stream);
 
@@ -70,6 +73,7 @@ int lsk_hip_tree_set_radii(float *nodes, int64_t n, const float *d2_sorted, void
 typedef struct lsk_tree_view {
   const float *pts;    // sorted points (padded)
   const float *nodes;  // node array
+  const float *qnodes; // quarter boxes (row kernel)
   int64_t n;
   int32_t depth;
   int32_t pad;
@@ -93,7 +97,8 @@ typedef struct lsk_knn_args {
   int32_t pad0;
 } lsk_knn_args;
 
-int lsk_hip_knn(const lsk_knn_args *args, void *stream);
+int lsk_hip_knn(const lsk_knn_args *args, void *stream);       // 64-query group kernel
+int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream);  // 4 x 16-query rows (default)
 
 // ---- halo exchange -------------------------------------------------------------------
 // Published tree: the top `levels` levels of a tree (node slots 1 .. 2^levels-1... up to

@@ -11,8 +11,22 @@
 
 namespace {
 
+__device__ __forceinline__ float min16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float max16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// One wave per 64-point bucket: the leaf box and (optionally) the four 16-point
+// quarter boxes used for per-row culling by the k-NN kernel.
 __global__ __launch_bounds__(256) void leaf_kernel(const float *__restrict__ pts, int64_t n,
-                                                   float *__restrict__ nodes, int depth,
+                                                   float *__restrict__ nodes,
+                                                   float *__restrict__ qnodes, int depth,
                                                    int64_t nleaf_slots) {
   const int64_t leaf = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (leaf >= nleaf_slots) return;
@@ -24,6 +38,14 @@ __global__ __launch_bounds__(256) void leaf_kernel(const float *__restrict__ pts
     lx = hx = pts[3 * i];
     ly = hy = pts[3 * i + 1];
     lz = hz = pts[3 * i + 2];
+  }
+  // quarter (16-lane row) boxes first, then the bucket box from them
+  lx = min16(lx); ly = min16(ly); lz = min16(lz);
+  hx = max16(hx); hy = max16(hy); hz = max16(hz);
+  if (qnodes && (lane & 15) == 0) {
+    float4 *qd = (float4 *)qnodes + 2 * (leaf * 4 + (lane >> 4));
+    qd[0] = make_float4(lx, ly, lz, 0.f);
+    qd[1] = make_float4(hx, hy, hz, 0.f);
   }
   lx = lsk::wave_min(lx); ly = lsk::wave_min(ly); lz = lsk::wave_min(lz);
   hx = lsk::wave_max(hx); hy = lsk::wave_max(hy); hz = lsk::wave_max(hz);
@@ -77,11 +99,11 @@ extern "C" int64_t lsk_hip_tree_nodes(int64_t n) {
 }
 
 extern "C" int lsk_hip_build_tree(const float *sorted_pts, int64_t n, float *nodes,
-                                  void *stream) {
+                                  float *qnodes, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   const int depth = lsk_hip_tree_depth(n);
   const int64_t slots = (int64_t)1 << depth;
-  leaf_kernel<<<lsk_blocks(slots, 4), 256, 0, s>>>(sorted_pts, n, nodes, depth, slots);
+  leaf_kernel<<<lsk_blocks(slots, 4), 256, 0, s>>>(sorted_pts, n, nodes, qnodes, depth, slots);
   LSK_CHECK_LAUNCH("tree_leaf");
   for (int l = depth - 1; l >= 0; l--) {
     levelup_kernel<<<lsk_blocks((int64_t)1 << l, 256), 256, 0, s>>>(nodes, l, 0);

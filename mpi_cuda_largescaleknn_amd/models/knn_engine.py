@@ -30,6 +30,7 @@ def cut2_of(max_radius: float) -> float:
 
 
 SEED_BUCKETS = 2  # Morton-neighbour buckets (each side) that seed the first pass
+KNN_IMPL = "rows"  # "rows" (4 x 16-query rows, quarter culling) or "wave" (64-query groups)
 
 
 @dataclass
@@ -50,6 +51,7 @@ class LocalIndex:
     pts: torch.Tensor        # [n + PAD, 3] Morton-sorted points (padded)
     perm: torch.Tensor       # int32 [n]: sorted position -> row of the input array
     nodes: torch.Tensor      # [2^(depth+1), 8] bucket-tree node boxes (lo.w = radius²)
+    qnodes: torch.Tensor     # [2^depth * 4, 8] boxes of each bucket's four 16-point quarters
     depth: int
     box: torch.Tensor        # [8] cube used for the Morton keys
 
@@ -58,7 +60,7 @@ class LocalIndex:
         return self.pts.device
 
     def tree(self) -> tuple:
-        return (self.pts, self.nodes, self.n, self.depth)
+        return (self.pts, self.nodes, self.qnodes, self.n, self.depth)
 
 
 @dataclass
@@ -68,7 +70,7 @@ class KnnStats:
     def add(self, raw: torch.Tensor) -> None:
         names = ["evals", "leaves", "nodes", "hist_passes", "overflow_lanes", "underflow_lanes",
                  "refine_lanes", "mismatch_lanes", "pass_limit_waves", "list_invalid_waves", "waves",
-                 "hint_lanes", "recorded_leaves"]
+                 "hint_lanes", "recorded_leaves", "collect_steps", "collect_nodes", "guard_trips"]
         vals = raw.cpu().tolist()
         for i, nm in enumerate(names):
             self.counters[nm] = self.counters.get(nm, 0) + int(vals[i])
@@ -84,8 +86,8 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None) -> LocalI
     keys, iota = K.morton(points, box)
     _, perm = K.sort_pairs(keys, iota, 30)
     pts = K.gather3(points, perm, pad=K.PAD_POINTS)
-    nodes, depth = K.build_tree(pts, n)
-    return LocalIndex(n, pts, perm, nodes, depth, box)
+    nodes, qnodes, depth = K.build_tree(pts, n)
+    return LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
 
 
 def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:
@@ -120,7 +122,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalInd
         trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
         raw = torch.zeros(16, dtype=torch.int64, device=index.device) if stats is not None else None
         K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
-                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS)
+                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL)
         if stats is not None:
             stats.add(raw)
         return out

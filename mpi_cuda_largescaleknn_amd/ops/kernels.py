@@ -150,20 +150,25 @@ def tree_depth(n: int) -> int:
     return d
 
 
-def build_tree(sorted_pts: torch.Tensor, n: int) -> tuple[torch.Tensor, int]:
-    """Bucket tree over the first n rows of sorted_pts -> (nodes [2^(D+1), 8], depth)."""
+def build_tree(sorted_pts: torch.Tensor, n: int) -> tuple[torch.Tensor, torch.Tensor, int]:
+    """Bucket tree over the first n rows of sorted_pts -> (nodes [2^(D+1), 8],
+    quarter boxes [2^D * 4, 8], depth)."""
     depth = tree_depth(n)
     slots = 1 << depth
     if is_gpu(sorted_pts):
         nodes = torch.empty((2 * slots, 8), dtype=torch.float32, device=sorted_pts.device)
-        check(_native.hip().lsk_hip_build_tree(_ptr(sorted_pts), n, _ptr(nodes), _stream(sorted_pts)),
-              "build_tree")
-        return nodes, depth
+        qnodes = torch.empty((4 * slots, 8), dtype=torch.float32, device=sorted_pts.device)
+        check(_native.hip().lsk_hip_build_tree(_ptr(sorted_pts), n, _ptr(nodes), _ptr(qnodes),
+                                               _stream(sorted_pts)), "build_tree")
+        return nodes, qnodes, depth
     inf = float("inf")
     lo = torch.full((slots * BUCKET, 3), inf)
     hi = torch.full((slots * BUCKET, 3), -inf)
     lo[:n] = sorted_pts[:n]
     hi[:n] = sorted_pts[:n]
+    qnodes = torch.zeros((4 * slots, 8), dtype=torch.float32)
+    qnodes[:, 0:3] = lo.view(4 * slots, 16, 3).amin(dim=1)
+    qnodes[:, 4:7] = hi.view(4 * slots, 16, 3).amax(dim=1)
     nodes = torch.zeros((2 * slots, 8), dtype=torch.float32)
     nodes[slots:, 0:3] = lo.view(slots, BUCKET, 3).amin(dim=1)
     nodes[slots:, 4:7] = hi.view(slots, BUCKET, 3).amax(dim=1)
@@ -173,7 +178,7 @@ def build_tree(sorted_pts: torch.Tensor, n: int) -> tuple[torch.Tensor, int]:
         nodes[a:2 * a, 0:3] = torch.minimum(ch[:, 0, 0:3], ch[:, 1, 0:3])
         nodes[a:2 * a, 4:7] = torch.maximum(ch[:, 0, 4:7], ch[:, 1, 4:7])
         nodes[a:2 * a, 3] = torch.maximum(ch[:, 0, 3], ch[:, 1, 3])
-    return nodes, depth
+    return nodes, qnodes, depth
 
 
 def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torch.Tensor:
@@ -198,10 +203,11 @@ def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torc
 def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hint2: float,
             out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
-            seed: int = 0) -> torch.Tensor:
+            seed: int = 0, impl: str = "rows") -> torch.Tensor:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
-    trees: list of (sorted_pts_padded, nodes, n, depth). seed > 0 declares that the
+    trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (4 x 16-query
+    rows with per-row quarter culling, default) or "wave" (64-query groups). seed > 0 declares that the
     queries are trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
     """
     a = KnnArgs()
@@ -209,8 +215,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     a.nq = nq
     a.groups = _ptr(groups)
     a.ngroups = ngroups
-    for i, (pts, nodes, n, depth) in enumerate(trees):
-        a.tree[i] = TreeView(_ptr(pts), _ptr(nodes), n, depth, 0)
+    for i, (pts, nodes, qnodes, n, depth) in enumerate(trees):
+        a.tree[i] = TreeView(_ptr(pts), _ptr(nodes), _ptr(qnodes), n, depth, 0)
     a.ntrees = len(trees)
     a.k = k
     a.cut2 = cut2
@@ -219,7 +225,9 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     a.stats = _ptr(stats)
     a.qstatus = _ptr(qstatus)
     a.seed = seed
-    check(_native.hip().lsk_hip_knn(C.byref(a), _stream(qpts)), "knn")
+    lib = _native.hip()
+    fn = lib.lsk_hip_knn_rows if impl == "rows" else lib.lsk_hip_knn
+    check(fn(C.byref(a), _stream(qpts)), "knn")
     return out_d2
 
 

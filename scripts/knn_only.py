@@ -12,10 +12,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--points", type=float, default=1e8)
 ap.add_argument("--k", type=int, default=100)
 ap.add_argument("--reps", type=int, default=1)
+ap.add_argument("--impl", default="rows")
 a = ap.parse_args()
 n = int(a.points)
 g = torch.Generator(device="cuda").manual_seed(1)
 p = torch.rand((n, 3), generator=g, device="cuda")
+E.KNN_IMPL = a.impl
 idx = E.build_index(p)
 cfg = E.KnnConfig(k=a.k)
 hint2 = E.radius_hint2(idx.box, n, a.k)
@@ -25,4 +27,4 @@ for r in range(a.reps):
     st = E.KnnStats()
     d2 = E.query(idx, cfg, hint2, stats=st if r == 0 else None)
     torch.cuda.synchronize()
-    print(f"knn {n} pts k={a.k}: {time.perf_counter() - t:.3f} s", st.counters, flush=True)
+    print(f"[{a.impl}] knn {n} pts k={a.k}: {time.perf_counter() - t:.3f} s", st.counters, flush=True)

@@ -80,11 +80,14 @@ def test_tree_build_matches_cpu(n):
     assert torch.equal(ig.pts[:n].cpu(), idx.pts[:n])
     assert ig.depth == idx.depth
     assert torch.equal(ig.nodes.cpu()[1:], idx.nodes[1:])
+    assert torch.equal(ig.qnodes.cpu()[:, [0, 1, 2, 4, 5, 6]], idx.qnodes[:, [0, 1, 2, 4, 5, 6]])
 
 
+@pytest.mark.parametrize("impl", ["rows", "wave"])
 @pytest.mark.parametrize("dist", list(GENERATORS))
 @pytest.mark.parametrize("k", [1, 8, 16, 100])
-def test_knn_matches_oracle(dist, k):
+def test_knn_matches_oracle(dist, k, impl, monkeypatch):
+    monkeypatch.setattr(E, "KNN_IMPL", impl)
     p = GENERATORS[dist](30000, seed=k)
     ref = oracle(p, k)
     stats = E.KnnStats()
@@ -139,3 +142,30 @@ def test_knn_large_uniform_brute_sample():
     idx = torch.randint(0, n, (2000,), generator=torch.Generator().manual_seed(1))
     ref = K.finalize_distances(K.kth_cpu(p, p[idx], 100, math.inf, "brute"))
     assert torch.equal(got[idx], ref)
+
+
+@pytest.mark.parametrize("impl", ["rows", "wave"])
+@pytest.mark.parametrize("k", [1, 16, 100])
+def test_knn_two_trees_and_groups(impl, k, monkeypatch):
+    """Queries of tree 0 against tree 0 + an overlapping second tree (the halo re-query
+    shape), for all groups and for a group subset."""
+    monkeypatch.setattr(E, "KNN_IMPL", impl)
+    a = uniform(30000, seed=k)
+    b = uniform(9000, seed=k + 100) * 0.5 + 0.25
+    ia, ib = E.build_index(a.to(DEV)), E.build_index(b.to(DEV))
+    cfg = E.KnnConfig(k=k)
+    hint2 = E.radius_hint2(ia.box, a.shape[0], k)
+    qs = ia.pts[:ia.n].cpu()
+    ref = K.kth_cpu(torch.cat([a, b]), qs, k, math.inf)
+    got = E.query(ia, cfg, hint2, extra=ib).cpu()
+    assert torch.equal(got, ref)
+    ngroups = (ia.n + 63) // 64
+    groups = torch.arange(1, ngroups, 3, dtype=torch.int32)
+    out = torch.full((ia.n,), -1.0, device=DEV)
+    E.query(ia, cfg, hint2, extra=ib, groups=groups.to(DEV), ngroups=groups.numel(), out=out)
+    sel = torch.zeros(ia.n, dtype=torch.bool)
+    for g in groups.tolist():
+        sel[g * 64:(g + 1) * 64] = True
+    out = out.cpu()
+    assert torch.equal(out[sel], ref[sel])
+    assert bool((out[~sel] == -1.0).all())
