@@ -177,3 +177,18 @@ def test_peer_choose_matches_reference_rule():
                 continue
             best, closest = peer, d
         assert got == best
+
+
+def test_native_host_unit_tests(tmp_path):
+    """The C++ host unit-test binary (CTest target host_tests) builds and passes."""
+    import subprocess
+
+    from mpi_cuda_largescaleknn_amd import _build
+    lib = _build.build_host()
+    src = os.path.join(_build.CSRC, "tests", "host_tests.cpp")
+    exe = str(tmp_path / "host_tests")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(_build.CSRC, "host"),
+                    src, "-o", exe, lib, f"-Wl,-rpath,{os.path.dirname(lib)}"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "host tests passed" in r.stdout
