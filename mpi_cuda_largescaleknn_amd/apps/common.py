@@ -54,6 +54,20 @@ def now(launch: Launch) -> float:
     return time.perf_counter()
 
 
+def guarded(launch: Launch, fn) -> int:
+    """Run fn(); any error on this rank is reported and broadcast to the peers (whose
+    watchdogs then abort) and the process exits 1 — a failing rank never leaves the
+    others blocked in a collective (parallel/faults.py)."""
+    try:
+        return fn()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 - every failure ends the job, loudly
+        from ..parallel import launch as L
+        L.fail(launch, e)
+        return 1
+
+
 def fail(msg: str, code: int = 1) -> None:
     sys.stderr.write(msg + "\n")
     sys.exit(code)

@@ -33,6 +33,10 @@ def main(argv: list[str] | None = None) -> int:
         common.fail("Error: --mode ring applies to hipKNN_unorderedData")
     names = io.read_file_list(args.input)
     launch = L.init(args.device, args.gpu_affinity, args.verbose)
+    return common.guarded(launch, lambda: _run(args, launch, names))
+
+
+def _run(args, launch, names) -> int:
     if launch.size != len(names):
         raise RuntimeError("number of input files does not match MPI size")
     pts = io.read_points(names[launch.rank], pin_memory=launch.device.type == "cuda")

@@ -30,6 +30,10 @@ def main(argv: list[str] | None = None) -> int:
     if args.mode == "peer":
         common.fail("Error: --mode peer applies to hipKNN_prePartitionedData")
     launch = L.init(args.device, args.gpu_affinity, args.verbose)
+    return common.guarded(launch, lambda: _run(args, launch))
+
+
+def _run(args, launch) -> int:
     pts, begin, total = io.read_portion(args.input, launch.rank, launch.size,
                                         pin_memory=launch.device.type == "cuda")
     print(f"#{launch.rank}/{launch.size}: got {pts.shape[0]} points to work on", flush=True)

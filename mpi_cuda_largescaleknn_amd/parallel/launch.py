@@ -16,12 +16,14 @@ unorderedDataVariant.cu:138-143); without ``-g`` the local rank picks the device
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
 
+from . import faults as F
 from .comm import Comm, SingleComm, TorchComm
 
 
@@ -32,6 +34,8 @@ class Launch:
     local_rank: int
     device: torch.device
     comm: Comm
+    store: object = None
+    watchdog: F.Watchdog | None = None
 
 
 def _env_int(*names, default=None):
@@ -58,21 +62,47 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         device = torch.device("cuda", dev_id)
     else:
         device = torch.device("cpu")
+    fault = F.parse_fault(os.environ.get("LSKNN_FAULT"))
+    store = watchdog = None
     if size > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(size)
+        # collective timeout = watchdog timeout; RCCL errors surface asynchronously
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        timeout = datetime.timedelta(seconds=F.timeout_s())
         if use_gpu:
-            dist.init_process_group("nccl", rank=rank, world_size=size, device_id=device)
+            dist.init_process_group("nccl", rank=rank, world_size=size, device_id=device, timeout=timeout)
         else:
-            dist.init_process_group("gloo", rank=rank, world_size=size)
+            dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
         comm: Comm = TorchComm(device)
+        store = dist.distributed_c10d._get_default_store()
+        watchdog = F.Watchdog(rank, size, store).start()
     else:
         comm = SingleComm(device)
-    return Launch(rank, size, local, device, comm)
+    return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
 
 
 def finalize(launch: Launch) -> None:
+    # the watchdog stops first: peers leaving the final barrier early close the store
+    if launch.watchdog is not None:
+        launch.watchdog.stop()
     if launch.size > 1 and dist.is_initialized():
         launch.comm.barrier()
         dist.destroy_process_group()
+
+
+def fail(launch: Launch, exc: BaseException) -> None:
+    """Report a rank failure (stderr + abort broadcast to the peers) and end the
+    process with exit code 1 without running teardown that could block on a peer."""
+    import sys
+    import traceback
+
+    sys.stdout.flush()
+    msg = f"{type(exc).__name__}: {exc}"
+    sys.stderr.write(f"#{launch.rank}/{launch.size}: error: {msg}\n")
+    if os.environ.get("LSKNN_TRACEBACK"):
+        traceback.print_exception(exc)
+    sys.stderr.flush()
+    F.announce_failure(launch.store, launch.rank, launch.size, exc)
+    os._exit(1)

@@ -32,6 +32,7 @@ import torch
 from ..models import knn_engine as E
 from ..ops import kernels as K
 from .comm import Comm
+from .faults import HEARTBEAT
 
 SPLIT_BITS = 16  # splitter resolution: top 16 of the 30 Morton bits
 
@@ -50,6 +51,7 @@ class PhaseTimer:
             self._t = time.perf_counter()
 
     def mark(self, name: str):
+        HEARTBEAT.beat(name)
         if self.enabled:
             self._sync()
             now = time.perf_counter()

@@ -1,0 +1,92 @@
+"""Failure detection and fault injection (SURVEY §5.3, §4.2 "Fault injection"): a rank
+that fails, crashes or hangs must end the whole job with a non-zero exit status and a
+message, and no rank may stay blocked. CPU, gloo, 2-3 processes via torchrun."""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+from mpi_cuda_largescaleknn_amd.parallel import faults as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+UN = "mpi_cuda_largescaleknn_amd.apps.unordered"
+PRE = "mpi_cuda_largescaleknn_amd.apps.prepartitioned"
+TOOLS = "mpi_cuda_largescaleknn_amd.apps.tools"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, nproc, env_extra=None, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(env_extra or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m"] + args
+    t = time.monotonic()
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    return p, time.monotonic() - t
+
+
+@pytest.fixture(scope="module")
+def pts(tmp_path_factory):
+    d = tmp_path_factory.mktemp("faults")
+    f = d / "pts.float3"
+    subprocess.run([sys.executable, "-m", TOOLS, "gen", str(f), "-n", "6000", "--seed", "1"],
+                   env=dict(os.environ, PYTHONPATH=ROOT), check=True)
+    return f
+
+
+def test_parse_fault_spec():
+    assert F.parse_fault(None) is None
+    f = F.parse_fault("rank=1,op=alltoallv,call=2,kind=hang")
+    assert f == {"rank": 1, "op": "alltoallv", "call": 2, "kind": "hang"}
+    assert F.parse_fault("rank=0")["op"] == "*"
+    with pytest.raises(ValueError):
+        F.parse_fault("op=barrier")
+    with pytest.raises(ValueError):
+        F.parse_fault("rank=0,kind=explode")
+
+
+@pytest.mark.parametrize("kind,code", [("raise", 1), ("exit", 7)])
+def test_injected_failure_ends_job(pts, tmp_path, kind, code):
+    p, dt = _run([UN, str(pts), "-o", str(tmp_path / "o.float"), "-k", "8", "--device", "cpu"], 2,
+                 {"LSKNN_FAULT": f"rank=1,op=alltoallv,call=0,kind={kind}"})
+    assert p.returncode != 0
+    assert "injected fault" in p.stderr
+    assert "#1/2" in p.stderr
+    assert dt < 200
+
+
+def test_hang_is_caught_by_watchdog(pts, tmp_path):
+    p, dt = _run([UN, str(pts), "-o", str(tmp_path / "o.float"), "-k", "8", "--device", "cpu"], 2,
+                 {"LSKNN_FAULT": "rank=0,op=alltoallv,kind=hang", "LSKNN_TIMEOUT": "6"})
+    assert p.returncode != 0
+    assert "injected fault (hang)" in p.stderr
+    # whichever fires first: this rank's watchdog, or the peer's collective timeout
+    # (which then broadcasts its failure)
+    assert any(m in p.stderr for m in ("watchdog: no progress", "aborting", "#1/2: error"))
+    assert dt < 200
+
+
+def test_missing_input_file_on_one_rank(pts, tmp_path):
+    lst = tmp_path / "files.txt"
+    lst.write_text(f"{pts}\n{tmp_path / 'does_not_exist.float3'}\n")
+    p, dt = _run([PRE, str(lst), "-o", str(tmp_path / "out"), "-k", "8", "--device", "cpu"], 2)
+    assert p.returncode != 0
+    assert "#1/2: error:" in p.stderr
+    assert dt < 200
+
+
+def test_rank_count_mismatch_message(pts, tmp_path):
+    lst = tmp_path / "files.txt"
+    lst.write_text(f"{pts}\n")
+    p, _ = _run([PRE, str(lst), "-o", str(tmp_path / "out"), "-k", "8", "--device", "cpu"], 2)
+    assert p.returncode != 0
+    assert "number of input files does not match MPI size" in p.stderr
