@@ -31,6 +31,7 @@ from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm  # noqa: E402
+from mpi_cuda_largescaleknn_amd.utils import trace  # noqa: E402
 
 METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -92,6 +93,10 @@ def main():
     info_last = None
 
     def step():
+        with trace.range("lsknn:step"):
+            _step()
+
+    def _step():
         nonlocal info_last
         info = PL.RunInfo(PL.PhaseTimer(args.phases, device))
         pts = host_pts.to(device, non_blocking=True)

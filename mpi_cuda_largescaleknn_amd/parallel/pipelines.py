@@ -31,6 +31,7 @@ import torch
 
 from ..models import knn_engine as E
 from ..ops import kernels as K
+from ..utils import trace
 from .comm import Comm
 from .faults import HEARTBEAT
 
@@ -52,6 +53,7 @@ class PhaseTimer:
 
     def mark(self, name: str):
         HEARTBEAT.beat(name)
+        trace.mark("lsknn:" + name)
         if self.enabled:
             self._sync()
             now = time.perf_counter()

@@ -169,3 +169,14 @@ def test_knn_two_trees_and_groups(impl, k, monkeypatch):
     out = out.cpu()
     assert torch.equal(out[sel], ref[sel])
     assert bool((out[~sel] == -1.0).all())
+
+
+def test_repeat_runs_and_kernels_bitwise_identical(monkeypatch):
+    """Race check: repeated runs, and the two kNN kernels, give identical
+    bits (the result does not depend on scheduling, atomics or the SIMD decomposition)."""
+    p = GENERATORS["clustered"](200_000, seed=9).to(DEV)
+    outs = []
+    for impl in ["rows", "rows", "wave"]:
+        monkeypatch.setattr(E, "KNN_IMPL", impl)
+        outs.append(E.knn_distances(p, 32).cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

@@ -192,3 +192,11 @@ def test_native_host_unit_tests(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert "host tests passed" in r.stdout
+
+
+def test_roctx_trace_is_safe_without_profiler():
+    from mpi_cuda_largescaleknn_amd.utils import trace
+    assert isinstance(trace.available(), bool)
+    trace.mark("lsknn:test")
+    with trace.range("lsknn:test-range"):
+        pass
