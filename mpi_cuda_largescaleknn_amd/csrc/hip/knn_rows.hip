@@ -44,10 +44,20 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
 static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
 constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
-constexpr int kStackCap = 64;
 constexpr uint32_t kShift0 = 20;
 constexpr uint32_t kMaxPasses = 96;
 constexpr uint32_t kGuardRounds = 1u << 22;
+
+// LSK_PROFILE builds (tuning only) accumulate per-wave shader-clock cycles per activity
+// into stats[16..23]: proc hist, proc collect, traverse hist, traverse collect, replay
+// hist, replay collect, final select, whole wave.
+#ifdef LSK_PROFILE
+#define LSK_PT(v) const uint64_t v = __builtin_readcyclecounter()
+#define LSK_PADD(acc, t0) (acc) += __builtin_readcyclecounter() - (t0)
+#else
+#define LSK_PT(v)
+#define LSK_PADD(acc, t0)
+#endif
 constexpr uint32_t kInvalid = 0xffffffffu;
 constexpr uint32_t kUnknown = 0xffffffffu;
 
@@ -56,7 +66,6 @@ enum { MODE_HIST = 0, MODE_COLLECT = 1 };
 
 struct WaveLds {
   uint32_t pool[kPool];
-  uint32_t stack[kStackCap];
 };
 // + per-row quarter lists (RCAP entries per row), a kernel template parameter: it sets
 // the LDS footprint and so the occupancy
@@ -195,15 +204,17 @@ struct WaveCtx {
   int32_t seed;
   float cx, cy, cz;
   uint32_t len0, len1, len2, len3;  // row list lengths (wave-uniform)
+  uint32_t rlen;                    // this lane's row's length (per lane; no select chain:
+                                    // the compiler turns one into a scratch lookup table)
   uint32_t done;                    // lockstep steps already processed
   bool list_ok;
   uint32_t guard;  // watchdog trips of the walk (never expected; see traverse)
+#ifdef LSK_PROFILE
+  uint64_t prof[8];
+#endif
   uint32_t steps, quarters, nodes_visited, csteps, cnodes;
 };
 
-__device__ __forceinline__ uint32_t row_len(const WaveCtx &W, int row) {
-  return row == 0 ? W.len0 : row == 1 ? W.len1 : row == 2 ? W.len2 : W.len3;
-}
 __device__ __forceinline__ uint32_t max_len(const WaveCtx &W) {
   return max(max(W.len0, W.len1), max(W.len2, W.len3));
 }
@@ -238,7 +249,7 @@ __device__ __forceinline__ uint32_t load_quarter(const lsk_knn_args &A, uint32_t
 
 __device__ __forceinline__ uint32_t row_entry(const WaveCtx &W, uint32_t step) {
   const uint32_t v = W.rl[(uint32_t)W.row * W.rcap + min(step, W.rcap - 1u)];
-  return step < row_len(W, W.row) ? v : kInvalid;
+  return step < W.rlen ? v : kInvalid;
 }
 
 // Lockstep processing of steps [b, e): row r handles its list entry `step`.
@@ -297,32 +308,95 @@ __device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
          ((ballot & 0xffff00000000ull) ? 4u : 0u) | ((ballot & 0xffff000000000000ull) ? 8u : 0u);
 }
 
+// Append entry e to the lists of the rows in rowmask: the leader lane of each such row
+// writes at its row's length (one vector LDS store), the lengths stay scalar.
 __device__ __forceinline__ void rows_append(WaveCtx &W, uint32_t rowmask, uint32_t e) {
-  if (rowmask & 1u) { if (W.lane == 0) W.rl[0u * W.rcap + W.len0] = e; W.len0++; }
-  if (rowmask & 2u) { if (W.lane == 0) W.rl[1u * W.rcap + W.len1] = e; W.len1++; }
-  if (rowmask & 4u) { if (W.lane == 0) W.rl[2u * W.rcap + W.len2] = e; W.len2++; }
-  if (rowmask & 8u) { if (W.lane == 0) W.rl[3u * W.rcap + W.len3] = e; W.len3++; }
+  const uint32_t mine = (rowmask >> W.row) & 1u;
+  if ((W.lane & 15) == 0 && mine) W.rl[(uint32_t)W.row * W.rcap + W.rlen] = e;
+  W.rlen += mine;
+  W.len0 += rowmask & 1u;
+  W.len1 += (rowmask >> 1) & 1u;
+  W.len2 += (rowmask >> 2) & 1u;
+  W.len3 += (rowmask >> 3) & 1u;
   W.quarters += __popc(rowmask);
+}
+
+// Quarter boxes of up to kPend pre-leaf nodes (8 quarters = 64 floats each, one dword
+// per lane) are loaded together — one memory latency per batch instead of per node —
+// and broadcast with v_readlane for the per-row tests.
+constexpr uint32_t kPend = 4;
+
+__device__ __forceinline__ float lanef(float v, uint32_t l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+}
+
+// One pre-leaf node's 8 quarters, already loaded one float per lane in `blk`.
+template <int MODE>
+__device__ __forceinline__ void test_block(Lane &s, WaveCtx &W, float blk, uint32_t t, uint32_t q0,
+                                           uint32_t nquarters, int64_t skip_lo, int64_t skip_hi) {
+#pragma unroll
+  for (uint32_t j = 0; j < 8; j++) {
+    const uint32_t qid = q0 + j;
+    const int64_t b = (int64_t)(qid >> 2);
+    if (qid >= nquarters || (b >= skip_lo && b <= skip_hi)) continue;
+    const float lx = lanef(blk, 8 * j), ly = lanef(blk, 8 * j + 1), lz = lanef(blk, 8 * j + 2);
+    const float hx = lanef(blk, 8 * j + 4), hy = lanef(blk, 8 * j + 5), hz = lanef(blk, 8 * j + 6);
+    const uint64_t m = __ballot(box_needed<MODE>(s, lx, ly, lz, hx, hy, hz));
+    rows_append(W, row_bits(m), (t << 31) | qid);
+  }
+}
+
+// Pending pre-leaf nodes p0..p3 (first quarter ids; scalars, never an indexed array).
+template <int MODE>
+__device__ __forceinline__ void flush_pending(Lane &s, WaveCtx &W, const float *qf, uint32_t t,
+                                              uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3,
+                                              uint32_t npend, uint32_t nquarters, int64_t skip_lo,
+                                              int64_t skip_hi, uint32_t qfloats) {
+  const uint32_t l = (uint32_t)W.lane, last = qfloats - 1u;
+  // all loads first (one latency for the batch), then the tests
+  const float b0 = qf[min(p0 * 8u + l, last)];
+  const float b1 = qf[min((npend > 1 ? p1 : p0) * 8u + l, last)];
+  const float b2 = qf[min((npend > 2 ? p2 : p0) * 8u + l, last)];
+  const float b3 = qf[min((npend > 3 ? p3 : p0) * 8u + l, last)];
+  test_block<MODE>(s, W, b0, t, p0, nquarters, skip_lo, skip_hi);
+  if (npend > 1) test_block<MODE>(s, W, b1, t, p1, nquarters, skip_lo, skip_hi);
+  if (npend > 2) test_block<MODE>(s, W, b2, t, p2, nquarters, skip_lo, skip_hi);
+  if (npend > 3) test_block<MODE>(s, W, b3, t, p3, nquarters, skip_lo, skip_hi);
+}
+
+__device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preserving for v >= 0
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(v));
 }
 
 // Tree walk (wave-uniform DFS, near child first) building the per-row quarter lists,
 // alternating with lockstep processing of what every row has pending (one processing
-// call site per pass keeps the kernel's register allocation tight). Seeding: tree 0's
-// buckets [g-seed, g+seed] are queued for every row first and skipped by the walk.
-// A list that would overflow forces a drain and a reset (replay then disabled).
+// call site per pass keeps the kernel's register allocation tight).
+//  * 4-ary steps: a popped node at level l tests its four grandchildren (level l+2,
+//    contiguous in the implicit tree: one 128-byte scalar load) — half the dependent
+//    pop -> load -> test rounds of a binary walk; a binary step lands on level depth-1
+//    when needed. Nodes at level depth-1 test the 8 quarter boxes of their two buckets
+//    directly (one 256-byte load), so buckets are never pushed.
+//  * Seeding: tree 0's buckets [g-seed, g+seed] are queued for every row first and
+//    skipped by the walk.
+//  * A list that would overflow forces a drain and a reset (replay then disabled).
 template <int MODE>
-__device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
+__device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
   const lsk::vec3f q{s.qx, s.qy, s.qz};
   const lsk::vec3f c{W.cx, W.cy, W.cz};
-  W.len0 = W.len1 = W.len2 = W.len3 = 0;
+  W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
   W.done = 0;
   uint32_t t = 0, sp = 0;
+  // DFS stack in one VGPR (lane i = entry i; < 64 entries): v_readlane to pop, a
+  // lane select to push, instead of an LDS round trip per node
+  uint32_t stk = 0;
   bool started = false, finished = false;
   int32_t seed_d = W.seed > 0 ? 0 : -1;  // next seed distance (tree 0 only)
   lsk_tree_view T = pick_tree(A, 0);
-  uint32_t leaf0 = 0, nquarters = 0, nbuckets = 0;
+  uint32_t nquarters = 0, nbuckets = 0;
+  int32_t depth = 0;
   int64_t skip_lo = 1, skip_hi = 0;
   uint32_t fill_rounds = 0;
+  uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0, npend = 0;  // pending pre-leaf nodes
   while (!finished) {
     bool overflow = false;
     if (++fill_rounds > kGuardRounds) {  // watchdog: never spin on the GPU
@@ -331,7 +405,17 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
     }
     // ---- fill until every row has a batch pending, a list is nearly full or the walk ends
     for (;;) {
-      if (max_len(W) + 4u > W.rcap) {
+      // room for the pending batch (8 entries per node per row) plus one more node
+      const bool room_short = max_len(W) + 8u * (npend + 1u) > W.rcap;
+      if (npend && (npend == kPend || room_short || (started && sp == 0))) {
+        LSK_PT(tq0);  // the one flush site (keeps a single inlined copy)
+        flush_pending<MODE>(s, W, T.qnodes, t, p0, p1, p2, p3, npend, nquarters, skip_lo, skip_hi,
+                            32u << depth);
+        LSK_PADD(W.prof[4], tq0);
+        npend = 0;
+        continue;
+      }
+      if (room_short) {
         overflow = true;
         break;
       }
@@ -346,7 +430,7 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
           t++;
           continue;
         }
-        leaf0 = 1u << T.depth;
+        depth = T.depth;
         nquarters = (uint32_t)((T.n + 15) / 16);
         nbuckets = (uint32_t)((T.n + lsk::kBucket - 1) / lsk::kBucket);
         skip_lo = 1;
@@ -355,7 +439,7 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
           skip_lo = (int64_t)W.g - W.seed;
           skip_hi = (int64_t)W.g + W.seed;
         }
-        if (W.lane == 0) W.L->stack[0] = 1u;
+        stk = W.lane == 0 ? 1u : stk;
         sp = 1;
         started = true;
       }
@@ -371,59 +455,97 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
         seed_d = seed_d < W.seed ? seed_d + 1 : -1;
         continue;
       }
-      if (sp == 0) {
+      if (sp == 0) {  // (nothing pending here: flushed above)
         t++;
         started = false;
         continue;
       }
-      lsk::cfloat4_p nodes = lsk::as_const4(T.nodes);
       sp--;
-      const uint32_t node = lsk::uniform(W.L->stack[sp]);
+      const uint32_t node = __builtin_amdgcn_readlane(stk, (int)sp);
       W.nodes_visited++;
       if (MODE == MODE_COLLECT) W.cnodes++;
-      if (node >= leaf0) {
-        const uint32_t b = node - leaf0;
-        if (b >= nbuckets || ((int64_t)b >= skip_lo && (int64_t)b <= skip_hi)) continue;
-        lsk::cfloat4_p qnodes = lsk::as_const4(T.qnodes);
-#pragma unroll
-        for (uint32_t qq = 0; qq < 4; qq++) {
-          const uint32_t qid = b * 4 + qq;
-          if (qid >= nquarters) break;
-          const lsk::v4f lo = qnodes[2 * qid], hi = qnodes[2 * qid + 1];
-          const uint64_t m = __ballot(box_needed<MODE>(s, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z));
-          rows_append(W, row_bits(m), (t << 31) | qid);
-        }
+      const int32_t lvl = 31 - __clz(node);
+      if (lvl == depth - 1 || depth == 0) {  // two buckets = 8 quarters (depth 0: the root)
+        const uint32_t q0 = depth == 0 ? 0u : (node - (1u << lvl)) * 8u;
+        p0 = npend == 0 ? q0 : p0;
+        p1 = npend == 1 ? q0 : p1;
+        p2 = npend == 2 ? q0 : p2;
+        p3 = npend == 3 ? q0 : p3;
+        npend++;
         continue;
       }
+      LSK_PT(tn0);
+      lsk::cfloat4_p nodes = lsk::as_const4(T.nodes);
       const float lim = MODE == MODE_HIST ? hist_bound(s)
                                           : (s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f);
-      const lsk::v4f lo = nodes[2 * node], hi = nodes[2 * node + 1];
-      if (!__ballot(lsk::box_dist2(q, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}) < lim)) continue;
-      const uint32_t c0 = 2 * node, c1 = c0 + 1;
-      const lsk::v4f l0 = nodes[2 * c0], h0 = nodes[2 * c0 + 1];
-      const lsk::v4f l1 = nodes[2 * c1], h1 = nodes[2 * c1 + 1];
-      const bool n0 = __ballot(lsk::box_dist2(q, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z}) < lim) != 0;
-      const bool n1 = __ballot(lsk::box_dist2(q, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z}) < lim) != 0;
-      const float g0 = lsk::box_dist2(c, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z});
-      const float g1 = lsk::box_dist2(c, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z});
-      const bool first0 = g0 <= g1;
-      const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
-      const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
-      if (na) {
-        if (W.lane == 0) W.L->stack[sp] = a;
-        sp++;
+      if (lvl + 2 <= depth - 1) {
+        const uint32_t g0 = 4u * node;
+        // test the 4 grandchildren; key = (center distance bits & ~3) | index, so the
+        // nearest is pushed last (popped first); scalar variables only (no arrays: an
+        // array here ends up in scratch and makes the stack index divergent)
+        uint32_t need = 0, k0, k1, k2, k3;
+        {
+          const lsk::v4f lo = nodes[2 * g0], hi = nodes[2 * g0 + 1];
+          const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
+          need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 1u : 0u;
+          k0 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 0u;
+        }
+        {
+          const lsk::v4f lo = nodes[2 * g0 + 2], hi = nodes[2 * g0 + 3];
+          const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
+          need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 2u : 0u;
+          k1 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 1u;
+        }
+        {
+          const lsk::v4f lo = nodes[2 * g0 + 4], hi = nodes[2 * g0 + 5];
+          const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
+          need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 4u : 0u;
+          k2 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 2u;
+        }
+        {
+          const lsk::v4f lo = nodes[2 * g0 + 6], hi = nodes[2 * g0 + 7];
+          const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
+          need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 8u : 0u;
+          k3 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 3u;
+        }
+        need = (uint32_t)__builtin_amdgcn_readfirstlane((int)need);
+        // sorting network, descending (push far ... near)
+#define LSK_CSWAP(a, b)                 \
+  {                                     \
+    const uint32_t hi_ = max(a, b);     \
+    b = min(a, b);                      \
+    a = hi_;                            \
+  }
+        LSK_CSWAP(k0, k1) LSK_CSWAP(k2, k3) LSK_CSWAP(k0, k2) LSK_CSWAP(k1, k3) LSK_CSWAP(k1, k2)
+#undef LSK_CSWAP
+        if ((need >> (k0 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k0 & 3u) : stk;
+        if ((need >> (k1 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k1 & 3u) : stk;
+        if ((need >> (k2 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k2 & 3u) : stk;
+        if ((need >> (k3 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k3 & 3u) : stk;
+      } else {  // binary step onto level depth-1
+        const uint32_t c0 = 2 * node, c1 = c0 + 1;
+        const lsk::v4f l0 = nodes[2 * c0], h0 = nodes[2 * c0 + 1];
+        const lsk::v4f l1 = nodes[2 * c1], h1 = nodes[2 * c1 + 1];
+        const bool n0 = __ballot(lsk::box_dist2(q, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z}) < lim) != 0;
+        const bool n1 = __ballot(lsk::box_dist2(q, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z}) < lim) != 0;
+        const float e0 = lsk::box_dist2(c, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z});
+        const float e1 = lsk::box_dist2(c, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z});
+        const bool first0 = e0 <= e1;
+        const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
+        const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
+        if (na) stk = W.lane == (int)sp++ ? a : stk;
+        if (nbb) stk = W.lane == (int)sp++ ? bb : stk;
       }
-      if (nbb) {
-        if (W.lane == 0) W.L->stack[sp] = bb;
-        sp++;
-      }
+      LSK_PADD(W.prof[5], tn0);
     }
     // ---- drain (single processing call site)
     const uint32_t target = (finished || overflow) ? max_len(W) : min_len(W);
+    LSK_PT(tp0);
     process_steps<MODE>(s, W, A, W.done, target);
+    LSK_PADD(W.prof[MODE], tp0);
     W.done = target;
     if (overflow) {
-      W.len0 = W.len1 = W.len2 = W.len3 = 0;
+      W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
       W.done = 0;
       W.list_ok = false;
     }
@@ -432,9 +554,9 @@ __device__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
 
 // Filter + compact every row's recorded list (in place, lockstep), then process it.
 template <int MODE>
-__device__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
+__device__ __forceinline__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
   const uint32_t total = max_len(W);
-  uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+  uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, nr = 0;
   for (uint32_t st = 0; st < total; st++) {
     const uint32_t e = row_entry(W, st);
     bool keep = false;
@@ -445,12 +567,9 @@ __device__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
       keep = box_retained<MODE>(s, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
     }
     const uint32_t rb = row_bits(__ballot(keep));
-    // lane 16r holds row r's entry
-    if ((W.lane & 15) == 0) {
-      const uint32_t r = (uint32_t)W.row;
-      const uint32_t pos = r == 0 ? n0 : r == 1 ? n1 : r == 2 ? n2 : n3;
-      if ((rb >> r) & 1u) W.rl[r * W.rcap + pos] = e;
-    }
+    const uint32_t mine = (rb >> W.row) & 1u;  // row leaders compact in place
+    if ((W.lane & 15) == 0 && mine) W.rl[(uint32_t)W.row * W.rcap + nr] = e;
+    nr += mine;
     n0 += rb & 1u;
     n1 += (rb >> 1) & 1u;
     n2 += (rb >> 2) & 1u;
@@ -460,8 +579,11 @@ __device__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
   W.len1 = n1;
   W.len2 = n2;
   W.len3 = n3;
+  W.rlen = nr;
   W.done = 0;
+  LSK_PT(tp0);
   process_steps<MODE>(s, W, A, 0, max_len(W));
+  LSK_PADD(W.prof[MODE], tp0);
   W.done = max_len(W);
 }
 
@@ -540,10 +662,14 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
   W.k = k;
   W.g = g;
   W.seed = A.seed;
-  W.len0 = W.len1 = W.len2 = W.len3 = 0;
+  W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
   W.done = 0;
   W.list_ok = true;
   W.guard = 0;
+#ifdef LSK_PROFILE
+  for (int i = 0; i < 8; i++) W.prof[i] = 0;
+  LSK_PT(twave0);
+#endif
   W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
 
   Lane s;
@@ -621,10 +747,14 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
       for (int j = 0; j < kPool / lsk::kWave; j++) W.L->pool[j * lsk::kWave + lane] = 0u;
       if (first || !W.list_ok) {
         if (!first) W.list_ok = false;  // lists rebuilt as work queues only
+        LSK_PT(tt0);
         traverse<MODE_HIST>(s, W, A);
+        LSK_PADD(W.prof[2], tt0);
         if (!first) W.list_ok = false;
       } else {
+        LSK_PT(tr0);
         replay<MODE_HIST>(s, W, A);
+        LSK_PADD(W.prof[4], tr0);
       }
       first = false;
       bool ovf = false;
@@ -699,8 +829,11 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
     if (s.state != ST_READY) s.band_lo = s.band_w = 0;
     s.coff = pool_off;
     s.ccnt = 0;
+    LSK_PT(tc0);
     if (W.list_ok) replay<MODE_COLLECT>(s, W, A);
     else traverse<MODE_COLLECT>(s, W, A);
+    LSK_PADD(W.prof[W.list_ok ? 5 : 3], tc0);
+    LSK_PT(ts0);
     if (s.state == ST_READY) {
       qs |= QS_COLLECTED;
       if (s.ccnt != s.bc) qs |= QS_MISMATCH;
@@ -721,6 +854,7 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
         s.ans = 0x7fc00000u;
       }
     }
+    LSK_PADD(W.prof[6], ts0);
   }
 
   if (valid) {
@@ -728,6 +862,11 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
     if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
   }
 
+#ifdef LSK_PROFILE
+  LSK_PADD(W.prof[7], twave0);
+  if (A.stats && lane == 0)
+    for (int i = 0; i < 8; i++) atomicAdd(&A.stats[16 + i], (unsigned long long)W.prof[i]);
+#endif
   if (A.stats) {
     auto cnt = [&](uint32_t bit) {
       return (unsigned long long)__popcll(__ballot(valid && (qs & bit)));
@@ -782,12 +921,12 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   // LSK_ROWS_RCAP=256 selects the replaying variant (tuning experiments).
   static const int rcap = [] {
     const char *e = getenv("LSK_ROWS_RCAP");
-    return e ? atoi(e) : 32;
+    return e ? atoi(e) : 64;
   }();
   if (rcap == 256)
     knn_rows_kernel<256><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   else
-    knn_rows_kernel<32><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+    knn_rows_kernel<64><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   LSK_CHECK_LAUNCH("knn_rows");
   return 0;
 }

@@ -70,7 +70,10 @@ class KnnStats:
     def add(self, raw: torch.Tensor) -> None:
         names = ["evals", "leaves", "nodes", "hist_passes", "overflow_lanes", "underflow_lanes",
                  "refine_lanes", "mismatch_lanes", "pass_limit_waves", "list_invalid_waves", "waves",
-                 "hint_lanes", "recorded_leaves", "collect_steps", "collect_nodes", "guard_trips"]
+                 "hint_lanes", "recorded_leaves", "collect_steps", "collect_nodes", "guard_trips",
+                 # cycle profile (LSK_PROFILE kernel builds only)
+                 "prof_proc_hist", "prof_proc_collect", "prof_walk_hist", "prof_walk_collect",
+                 "prof_quarters", "prof_inner_nodes", "prof_select", "prof_wave"]
         vals = raw.cpu().tolist()
         for i, nm in enumerate(names):
             self.counters[nm] = self.counters.get(nm, 0) + int(vals[i])
@@ -120,7 +123,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalInd
         return out
     if K.is_gpu(index.pts):
         trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
-        raw = torch.zeros(16, dtype=torch.int64, device=index.device) if stats is not None else None
+        raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
         K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
                   stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL)
         if stats is not None:

@@ -28,3 +28,8 @@ for r in range(a.reps):
     d2 = E.query(idx, cfg, hint2, stats=st if r == 0 else None)
     torch.cuda.synchronize()
     print(f"[{a.impl}] knn {n} pts k={a.k}: {time.perf_counter() - t:.3f} s", st.counters, flush=True)
+    c = st.counters
+    if c.get("prof_wave"):
+        tot = c["prof_wave"]
+        print("  cycle profile (% of wave time):", {k[5:]: round(100.0 * v / tot, 1)
+                                                    for k, v in c.items() if k.startswith("prof_")}, flush=True)
