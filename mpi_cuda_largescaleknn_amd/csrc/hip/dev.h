@@ -28,20 +28,35 @@ __device__ __forceinline__ uint32_t uniform(uint32_t v) {
 }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Wave reductions. The result is equal in every lane; the final readfirstlane makes it
+// provably uniform (an SGPR): without it, control flow that depends on the value is
+// compiled as divergent (exec-masked loops, per-lane copies of scalar state).
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
-  return v;
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// K-th smallest (1-based) of a per-lane uint32 over the wave, by a bitwise ballot
+// search (32 rounds of compare + ballot + popcount); uniform result.
+__device__ __forceinline__ uint32_t wave_kth_smallest(uint32_t v, uint32_t K) {
+  uint32_t lo = 0;  // largest value with count(v < lo) < K
+#pragma unroll
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t cand = lo | (1u << b);
+    if ((uint32_t)__popcll(__ballot(v < cand)) < K) lo = cand;
+  }
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
 }
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5.5 T1): blocks are dealt

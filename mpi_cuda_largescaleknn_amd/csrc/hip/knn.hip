@@ -420,6 +420,16 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
   W.cz = 0.5f * (lz + hz);
 
   float r_est2 = own_group_estimate(s, nvalid, k);
+  {
+    // Robust cap: a group straddling a Morton discontinuity has lanes with few
+    // same-side neighbours in the group, whose estimate is then orders of magnitude too
+    // large (range far above the k-th value: huge first-pass bound, one slow wave).
+    // Cap at 16x (4 octaves of d2) the wave's lower-quartile estimate.
+    const bool ok = valid && r_est2 > 0.f && r_est2 < inf;
+    const uint32_t kq = max(1u, nvalid / 4u);
+    const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
+    if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
+  }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
     r_est2 = A.r_hint2;
     qs |= QS_HINT;

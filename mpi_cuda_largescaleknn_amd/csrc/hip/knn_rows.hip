@@ -36,14 +36,22 @@ using lsk::fbits;
 constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #ifndef LSK_ROWS_BINS
-#define LSK_ROWS_BINS 64
+#define LSK_ROWS_BINS 48
 #endif
 #ifndef LSK_ROWS_MINW
 #define LSK_ROWS_MINW 1
 #endif
+// 48 bins of 1/8 octave of d² (kShift0), initial range 4.5 octaves below / 1.5 above the
+// estimate: 6 KB of pool per wave -> 5 waves/SIMD (64 bins: 8 KB, 4 waves/SIMD, 15 %
+// slower; 32 bins: too many refine passes). Measured on 1e8 uniform points, k=100.
 constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
 static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
 constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
+#ifndef LSK_TOP_BINS
+#define LSK_TOP_BINS 12
+#endif
+constexpr int kTopBins = LSK_TOP_BINS;  // bins of the initial range above the estimate
+constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(log2(kBins))
 constexpr uint32_t kShift0 = 20;
 constexpr uint32_t kMaxPasses = 96;
 constexpr uint32_t kGuardRounds = 1u << 22;
@@ -69,10 +77,16 @@ struct WaveLds {
 };
 // + per-row quarter lists (RCAP entries per row), a kernel template parameter: it sets
 // the LDS footprint and so the occupancy
+#ifndef LSK_LDS_PAD
+#define LSK_LDS_PAD 0
+#endif
 template <int RCAP>
 struct WaveLdsR {
   WaveLds w;
   uint32_t rl[4 * RCAP];
+#if LSK_LDS_PAD > 0
+  uint32_t pad[LSK_LDS_PAD];  // tuning experiments only
+#endif
 };
 
 struct Lane {
@@ -324,7 +338,10 @@ __device__ __forceinline__ void rows_append(WaveCtx &W, uint32_t rowmask, uint32
 // Quarter boxes of up to kPend pre-leaf nodes (8 quarters = 64 floats each, one dword
 // per lane) are loaded together — one memory latency per batch instead of per node —
 // and broadcast with v_readlane for the per-row tests.
-constexpr uint32_t kPend = 4;
+#ifndef LSK_PEND
+#define LSK_PEND 4
+#endif
+constexpr uint32_t kPend = LSK_PEND;  // 4 or 8
 
 __device__ __forceinline__ float lanef(float v, uint32_t l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
@@ -346,22 +363,31 @@ __device__ __forceinline__ void test_block(Lane &s, WaveCtx &W, float blk, uint3
   }
 }
 
-// Pending pre-leaf nodes p0..p3 (first quarter ids; scalars, never an indexed array).
+// Pending pre-leaf nodes p[0..kPend) (first quarter ids; scalars — an indexed array
+// would live in scratch).
+struct Pend {
+  uint32_t p0, p1, p2, p3, p4, p5, p6, p7, n;
+};
+
 template <int MODE>
 __device__ __forceinline__ void flush_pending(Lane &s, WaveCtx &W, const float *qf, uint32_t t,
-                                              uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3,
-                                              uint32_t npend, uint32_t nquarters, int64_t skip_lo,
+                                              const Pend &P, uint32_t nquarters, int64_t skip_lo,
                                               int64_t skip_hi, uint32_t qfloats) {
   const uint32_t l = (uint32_t)W.lane, last = qfloats - 1u;
   // all loads first (one latency for the batch), then the tests
-  const float b0 = qf[min(p0 * 8u + l, last)];
-  const float b1 = qf[min((npend > 1 ? p1 : p0) * 8u + l, last)];
-  const float b2 = qf[min((npend > 2 ? p2 : p0) * 8u + l, last)];
-  const float b3 = qf[min((npend > 3 ? p3 : p0) * 8u + l, last)];
-  test_block<MODE>(s, W, b0, t, p0, nquarters, skip_lo, skip_hi);
-  if (npend > 1) test_block<MODE>(s, W, b1, t, p1, nquarters, skip_lo, skip_hi);
-  if (npend > 2) test_block<MODE>(s, W, b2, t, p2, nquarters, skip_lo, skip_hi);
-  if (npend > 3) test_block<MODE>(s, W, b3, t, p3, nquarters, skip_lo, skip_hi);
+#define LSK_LD(i) const float b##i = qf[min((P.n > i ? P.p##i : P.p0) * 8u + l, last)];
+  LSK_LD(0) LSK_LD(1) LSK_LD(2) LSK_LD(3)
+#if LSK_PEND > 4
+  LSK_LD(4) LSK_LD(5) LSK_LD(6) LSK_LD(7)
+#endif
+#undef LSK_LD
+#define LSK_TB(i) \
+  if (P.n > i) test_block<MODE>(s, W, b##i, t, P.p##i, nquarters, skip_lo, skip_hi);
+  LSK_TB(0) LSK_TB(1) LSK_TB(2) LSK_TB(3)
+#if LSK_PEND > 4
+  LSK_TB(4) LSK_TB(5) LSK_TB(6) LSK_TB(7)
+#endif
+#undef LSK_TB
 }
 
 __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preserving for v >= 0
@@ -396,7 +422,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   int32_t depth = 0;
   int64_t skip_lo = 1, skip_hi = 0;
   uint32_t fill_rounds = 0;
-  uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0, npend = 0;  // pending pre-leaf nodes
+  Pend P{0, 0, 0, 0, 0, 0, 0, 0, 0};  // pending pre-leaf nodes
   while (!finished) {
     bool overflow = false;
     if (++fill_rounds > kGuardRounds) {  // watchdog: never spin on the GPU
@@ -406,13 +432,12 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     // ---- fill until every row has a batch pending, a list is nearly full or the walk ends
     for (;;) {
       // room for the pending batch (8 entries per node per row) plus one more node
-      const bool room_short = max_len(W) + 8u * (npend + 1u) > W.rcap;
-      if (npend && (npend == kPend || room_short || (started && sp == 0))) {
+      const bool room_short = max_len(W) + 8u * (P.n + 1u) > W.rcap;
+      if (P.n && (P.n == kPend || room_short || (started && sp == 0))) {
         LSK_PT(tq0);  // the one flush site (keeps a single inlined copy)
-        flush_pending<MODE>(s, W, T.qnodes, t, p0, p1, p2, p3, npend, nquarters, skip_lo, skip_hi,
-                            32u << depth);
+        flush_pending<MODE>(s, W, T.qnodes, t, P, nquarters, skip_lo, skip_hi, 32u << depth);
         LSK_PADD(W.prof[4], tq0);
-        npend = 0;
+        P.n = 0;
         continue;
       }
       if (room_short) {
@@ -467,11 +492,17 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
       const int32_t lvl = 31 - __clz(node);
       if (lvl == depth - 1 || depth == 0) {  // two buckets = 8 quarters (depth 0: the root)
         const uint32_t q0 = depth == 0 ? 0u : (node - (1u << lvl)) * 8u;
-        p0 = npend == 0 ? q0 : p0;
-        p1 = npend == 1 ? q0 : p1;
-        p2 = npend == 2 ? q0 : p2;
-        p3 = npend == 3 ? q0 : p3;
-        npend++;
+        P.p0 = P.n == 0 ? q0 : P.p0;
+        P.p1 = P.n == 1 ? q0 : P.p1;
+        P.p2 = P.n == 2 ? q0 : P.p2;
+        P.p3 = P.n == 3 ? q0 : P.p3;
+        if (kPend > 4) {
+          P.p4 = P.n == 4 ? q0 : P.p4;
+          P.p5 = P.n == 5 ? q0 : P.p5;
+          P.p6 = P.n == 6 ? q0 : P.p6;
+          P.p7 = P.n == 7 ? q0 : P.p7;
+        }
+        P.n++;
         continue;
       }
       LSK_PT(tn0);
@@ -530,7 +561,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         const bool n1 = __ballot(lsk::box_dist2(q, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z}) < lim) != 0;
         const float e0 = lsk::box_dist2(c, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z});
         const float e1 = lsk::box_dist2(c, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z});
-        const bool first0 = e0 <= e1;
+        const bool first0 = ubits(e0) <= ubits(e1);  // uniform
         const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
         const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
         if (na) stk = W.lane == (int)sp++ ? a : stk;
@@ -687,6 +718,16 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
   W.cz = 0.5f * (lz + hz);
 
   float r_est2 = own_group_estimate(s, nvalid, k);
+  {
+    // Robust cap: a group straddling a Morton discontinuity has lanes with few
+    // same-side neighbours in the group, whose estimate is then orders of magnitude too
+    // large (range far above the k-th value: huge first-pass bound, one slow wave).
+    // Cap at 16x (4 octaves of d2) the wave's lower-quartile estimate.
+    const bool ok = valid && r_est2 > 0.f && r_est2 < inf;
+    const uint32_t kq = max(1u, nvalid / 4u);
+    const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
+    if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
+  }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
     r_est2 = A.r_hint2;
     qs |= QS_HINT;
@@ -715,7 +756,7 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
   } else {
     s.state = ST_HIST;
     const uint32_t est_b = fbits(r_est2);
-    const uint32_t off = (uint32_t)(kBins - 16) << kShift0;  // range top 2 octaves above
+    const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;  // range top kTopBins/8 octaves above
     const uint32_t lo0 = est_b > off ? est_b - off : 0u;
     set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
   }
@@ -817,7 +858,7 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
     if (total <= (uint32_t)kPool) break;
     if (s.state == ST_READY && s.bc > (uint32_t)(kPool / lsk::kWave)) {
       qs |= QS_REFINE;
-      const uint32_t sh = s.shift >= 6u ? s.shift - 6u : 0u;
+      const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;  // kBins bins cover the band
       set_range(s, s.band_lo, sh, s.band_lo + s.band_w, k - s.m);
       s.band_lo = s.band_w = 0;
       s.state = ST_HIST;
@@ -859,7 +900,12 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
 
   if (valid) {
     A.out_d2[qi] = bitsf(s.ans);
+#ifdef LSK_PROFILE  // debug: wave cycles (>> 16) in place of the pass count
+    if (A.qstatus)
+      A.qstatus[qi] = qs | ((uint32_t)min((__builtin_readcyclecounter() - twave0) >> 16, (uint64_t)0xffff) << 16);
+#else
     if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
+#endif
   }
 
 #ifdef LSK_PROFILE
@@ -915,18 +961,19 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
   const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
-  // Row-list capacity: 32 entries keeps the block at 35 KB of LDS (4 waves/SIMD) and
-  // uses the lists only as per-pass work queues; 256 also replays them across passes but
-  // costs one wave/SIMD of occupancy (measured slower: 0.52 vs 0.46 s, 1e8 pts, k=100).
-  // LSK_ROWS_RCAP=256 selects the replaying variant (tuning experiments).
+  // Row-list capacity: 32 entries per row keeps the block at 26 KB of LDS (5 waves/SIMD);
+  // the lists are per-pass work queues. 256 also replays them across passes but costs
+  // occupancy (measured slower). LSK_ROWS_RCAP=64/256 select other instances (tuning).
   static const int rcap = [] {
     const char *e = getenv("LSK_ROWS_RCAP");
-    return e ? atoi(e) : 64;
+    return e ? atoi(e) : 32;
   }();
   if (rcap == 256)
     knn_rows_kernel<256><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
-  else
+  else if (rcap == 64)
     knn_rows_kernel<64><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+  else
+    knn_rows_kernel<32><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   LSK_CHECK_LAUNCH("knn_rows");
   return 0;
 }
