@@ -6,26 +6,31 @@
 // unorderedDataVariant.cu:75-103), with a different SIMD decomposition:
 //
 //  * a wave owns 64 consecutive Morton-sorted queries split into 4 ROWS of 16 (the
-//    16-lane rows of CDNA4 DPP). The tree walk is still wave-uniform (LDS stack, scalar
-//    node loads), but at a 64-point leaf each row tests the leaf's four 16-point QUARTER
-//    boxes with its own 16 lanes and appends the quarters it needs to its own LDS list;
-//  * rows consume their lists in lockstep: one step = one quarter per row, the 16
+//    16-lane rows of CDNA4 DPP). The tree walk is wave-uniform (DFS with the stack in one
+//    VGPR, 4-ary steps over the implicit bucket tree, scalar node loads, near child
+//    first); at the level above the buckets each row tests the 8 16-point QUARTER boxes
+//    of the node's two buckets with its own 16 lanes and queues the quarters it needs.
+//    Quarter boxes of 4 such nodes are fetched with one vector load per node (one
+//    memory latency per batch) and broadcast with v_readlane;
+//  * rows consume their queues in lockstep: one step = one quarter per row, the 16
 //    candidates of each row's quarter are loaded by the row's 16 lanes (one vector load,
 //    prefetched one step ahead) and broadcast inside the row with DPP row_newbcast, which
 //    the compiler folds into v_subrev_f32_dpp — the broadcast costs nothing;
 //  * so a query evaluates only candidates of quarters its own 16-query row needs (small
 //    union of balls, 16-point culling granularity) instead of everything its 64-query
-//    group needs.
-//  * the walk and the processing alternate (fill the row lists until every row has a
-//    batch pending, then drain in lockstep), so each list is a short work queue. With a
-//    large capacity (RCAP=256) the lists recorded in pass 1 are also replayed (filtered +
-//    compacted per row) by the retry and collect passes, but the LDS that costs lowers
-//    occupancy by more than the replay saves; the default RCAP=32 re-walks each pass.
+//    group needs;
+//  * walk and processing alternate (fill the row queues until every row has a batch
+//    pending, then drain in lockstep); pass 1 logs the visited nodes with the rows that
+//    took each quarter (a private-memory log striped over the lanes), and the later
+//    passes (collect, retries) replay that log instead of walking the tree again;
 //  * histogram bin index = sat(d²bits - lo) >> shift: values below the range land in bin
-//    0 (no separate compare), and c_base tracks how many of them are known to be below.
+//    0 (no separate compare), and c_base tracks how many of them are known to be below;
+//  * the per-lane estimate that places the first range is capped by the wave's lower
+//    quartile: groups straddling a Morton discontinuity otherwise produce a few waves
+//    with absurd first-pass bounds that dominate the kernel's tail.
 //  Inner-loop cost per candidate and lane: 6 VALU for d² (DPP broadcast folded into the
 //  subtracts) + 8 VALU + 1 ds_add for the histogram (compiled with -fno-slp-vectorize:
-//  packed-math ops cannot take DPP operands).
+//  packed-math ops cannot take DPP operands). 6 waves/SIMD (80 VGPRs, 26 KB LDS/block).
 #include "dev.h"
 
 namespace {
@@ -39,7 +44,9 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #define LSK_ROWS_BINS 48
 #endif
 #ifndef LSK_ROWS_MINW
-#define LSK_ROWS_MINW 1
+// 6 waves/SIMD: LDS allows 6 (26 KB/block), the allocator lands at 83 VGPRs unless told
+// to fit 80 (5 spilled VGPRs; 0.248 vs 0.261 s, 1e8 pts, k=100)
+#define LSK_ROWS_MINW 6
 #endif
 // 48 bins of 1/8 octave of d² (kShift0), initial range 4.5 octaves below / 1.5 above the
 // estimate: 6 KB of pool per wave -> 5 waves/SIMD (64 bins: 8 KB, 4 waves/SIMD, 15 %
@@ -221,7 +228,11 @@ struct WaveCtx {
   uint32_t rlen;                    // this lane's row's length (per lane; no select chain:
                                     // the compiler turns one into a scratch lookup table)
   uint32_t done;                    // lockstep steps already processed
-  bool list_ok;
+  // pass-1 log of the visited pre-leaf nodes: entry n = (first quarter | tree << 31,
+  // 4 row bits per quarter) held by lane n % 64 of word n / 64 of two private arrays
+  uint32_t logn;
+  bool logging, log_ok;
+  uint32_t *logq, *logm;
   uint32_t guard;  // watchdog trips of the walk (never expected; see traverse)
 #ifdef LSK_PROFILE
   uint64_t prof[8];
@@ -338,35 +349,55 @@ __device__ __forceinline__ void rows_append(WaveCtx &W, uint32_t rowmask, uint32
 // Quarter boxes of up to kPend pre-leaf nodes (8 quarters = 64 floats each, one dword
 // per lane) are loaded together — one memory latency per batch instead of per node —
 // and broadcast with v_readlane for the per-row tests.
-#ifndef LSK_PEND
-#define LSK_PEND 4
-#endif
-constexpr uint32_t kPend = LSK_PEND;  // 4 or 8
+constexpr uint32_t kPend = 4;
+constexpr uint32_t kLogWords = 8;  // log capacity 512 pre-leaf entries (private memory)
+constexpr uint32_t kLogCap = kLogWords * 64;
 
 __device__ __forceinline__ float lanef(float v, uint32_t l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
 }
 
-// One pre-leaf node's 8 quarters, already loaded one float per lane in `blk`.
+// One pre-leaf node's 8 quarters, already loaded one float per lane in `blk`; lmask
+// restricts the rows per quarter (4 bits each; all ones for a walk). Returns the rows
+// that took each quarter (same layout).
 template <int MODE>
-__device__ __forceinline__ void test_block(Lane &s, WaveCtx &W, float blk, uint32_t t, uint32_t q0,
-                                           uint32_t nquarters, int64_t skip_lo, int64_t skip_hi) {
+__device__ __forceinline__ uint32_t test_block(Lane &s, WaveCtx &W, float blk, uint32_t t, uint32_t q0,
+                                               uint32_t lmask, uint32_t nquarters, int64_t skip_lo,
+                                               int64_t skip_hi) {
+  uint32_t took = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 8; j++) {
     const uint32_t qid = q0 + j;
     const int64_t b = (int64_t)(qid >> 2);
-    if (qid >= nquarters || (b >= skip_lo && b <= skip_hi)) continue;
+    const uint32_t lm = (lmask >> (4 * j)) & 0xfu;
+    if (lm == 0 || qid >= nquarters || (b >= skip_lo && b <= skip_hi)) continue;
     const float lx = lanef(blk, 8 * j), ly = lanef(blk, 8 * j + 1), lz = lanef(blk, 8 * j + 2);
     const float hx = lanef(blk, 8 * j + 4), hy = lanef(blk, 8 * j + 5), hz = lanef(blk, 8 * j + 6);
-    const uint64_t m = __ballot(box_needed<MODE>(s, lx, ly, lz, hx, hy, hz));
-    rows_append(W, row_bits(m), (t << 31) | qid);
+    const uint32_t rm = row_bits(__ballot(box_needed<MODE>(s, lx, ly, lz, hx, hy, hz))) & lm;
+    rows_append(W, rm, (t << 31) | qid);
+    took |= rm << (4 * j);
   }
+  return took;
+}
+
+__device__ __forceinline__ void log_put(WaveCtx &W, uint32_t e, uint32_t mask) {
+  if (W.logn >= kLogCap) {
+    W.log_ok = false;
+    return;
+  }
+  const uint32_t slot = W.logn >> 6;
+  if (W.lane == (int)(W.logn & 63u)) {
+    W.logq[slot] = e;
+    W.logm[slot] = mask;
+  }
+  W.logn++;
 }
 
 // Pending pre-leaf nodes p[0..kPend) (first quarter ids; scalars — an indexed array
 // would live in scratch).
 struct Pend {
-  uint32_t p0, p1, p2, p3, p4, p5, p6, p7, n;
+  uint32_t p0, p1, p2, p3, n;
+  uint32_t m0, m1, m2, m3;  // row masks (replay; all ones for a walk)
 };
 
 template <int MODE>
@@ -377,16 +408,14 @@ __device__ __forceinline__ void flush_pending(Lane &s, WaveCtx &W, const float *
   // all loads first (one latency for the batch), then the tests
 #define LSK_LD(i) const float b##i = qf[min((P.n > i ? P.p##i : P.p0) * 8u + l, last)];
   LSK_LD(0) LSK_LD(1) LSK_LD(2) LSK_LD(3)
-#if LSK_PEND > 4
-  LSK_LD(4) LSK_LD(5) LSK_LD(6) LSK_LD(7)
-#endif
 #undef LSK_LD
-#define LSK_TB(i) \
-  if (P.n > i) test_block<MODE>(s, W, b##i, t, P.p##i, nquarters, skip_lo, skip_hi);
+#define LSK_TB(i)                                                                          \
+  if (P.n > i) {                                                                           \
+    const uint32_t took = test_block<MODE>(s, W, b##i, t, P.p##i, P.m##i, nquarters, skip_lo, \
+                                           skip_hi);                                     \
+    if (W.logging && took) log_put(W, P.p##i | (t << 31), took);                           \
+  }
   LSK_TB(0) LSK_TB(1) LSK_TB(2) LSK_TB(3)
-#if LSK_PEND > 4
-  LSK_TB(4) LSK_TB(5) LSK_TB(6) LSK_TB(7)
-#endif
 #undef LSK_TB
 }
 
@@ -405,7 +434,10 @@ __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preservi
 //  * Seeding: tree 0's buckets [g-seed, g+seed] are queued for every row first and
 //    skipped by the walk.
 //  * A list that would overflow forces a drain and a reset (replay then disabled).
-template <int MODE>
+//  * replay (pass > 1 with a complete pass-1 log): the pre-leaf nodes and per-quarter
+//    row masks come from the log instead of the walk (bounds only shrink after pass 1,
+//    so the log is a superset of what later passes need).
+template <int MODE, bool replay>
 __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
   const lsk::vec3f q{s.qx, s.qy, s.qz};
   const lsk::vec3f c{W.cx, W.cy, W.cz};
@@ -422,7 +454,9 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   int32_t depth = 0;
   int64_t skip_lo = 1, skip_hi = 0;
   uint32_t fill_rounds = 0;
-  Pend P{0, 0, 0, 0, 0, 0, 0, 0, 0};  // pending pre-leaf nodes
+  Pend P{0, 0, 0, 0, 0, ~0u, ~0u, ~0u, ~0u};  // pending pre-leaf nodes
+  uint32_t ri = 0, lq = 0, lmk = 0;  // replay cursor, cached log words
+  if (!replay && W.logging) W.logn = 0;
   while (!finished) {
     bool overflow = false;
     if (++fill_rounds > kGuardRounds) {  // watchdog: never spin on the GPU
@@ -480,6 +514,29 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         seed_d = seed_d < W.seed ? seed_d + 1 : -1;
         continue;
       }
+      if (replay) {
+        if (ri >= W.logn) {  // (nothing pending here: flushed above)
+          finished = true;
+          break;
+        }
+        if ((ri & 63u) == 0) {  // next 64 log entries, one per lane
+          lq = W.logq[ri >> 6];
+          lmk = W.logm[ri >> 6];
+        }
+        const uint32_t e = __builtin_amdgcn_readlane(lq, (int)(ri & 63u));
+        const uint32_t mk = __builtin_amdgcn_readlane(lmk, (int)(ri & 63u));
+        // the logged rows per quarter are appended as they are: they are a superset of
+        // what any later pass needs (bounds only shrink), and skipping the re-test keeps
+        // replay free of box loads
+        const uint32_t tq = e & 0x80000000u, q0 = e & 0x7fffffffu;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+          const uint32_t rm = (mk >> (4 * j)) & 0xfu;
+          if (rm) rows_append(W, rm, tq | (q0 + j));
+        }
+        ri++;
+        continue;
+      }
       if (sp == 0) {  // (nothing pending here: flushed above)
         t++;
         started = false;
@@ -496,12 +553,6 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         P.p1 = P.n == 1 ? q0 : P.p1;
         P.p2 = P.n == 2 ? q0 : P.p2;
         P.p3 = P.n == 3 ? q0 : P.p3;
-        if (kPend > 4) {
-          P.p4 = P.n == 4 ? q0 : P.p4;
-          P.p5 = P.n == 5 ? q0 : P.p5;
-          P.p6 = P.n == 6 ? q0 : P.p6;
-          P.p7 = P.n == 7 ? q0 : P.p7;
-        }
         P.n++;
         continue;
       }
@@ -578,44 +629,8 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     if (overflow) {
       W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
       W.done = 0;
-      W.list_ok = false;
     }
   }
-}
-
-// Filter + compact every row's recorded list (in place, lockstep), then process it.
-template <int MODE>
-__device__ __forceinline__ void replay(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
-  const uint32_t total = max_len(W);
-  uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, nr = 0;
-  for (uint32_t st = 0; st < total; st++) {
-    const uint32_t e = row_entry(W, st);
-    bool keep = false;
-    if (e != kInvalid) {
-      const float *qn = (e >> 31) ? A.tree[1].qnodes : A.tree[0].qnodes;  // per-lane select
-      const float4 *qb = (const float4 *)qn + 2 * (size_t)(e & 0x7fffffffu);
-      const float4 lo = qb[0], hi = qb[1];
-      keep = box_retained<MODE>(s, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
-    }
-    const uint32_t rb = row_bits(__ballot(keep));
-    const uint32_t mine = (rb >> W.row) & 1u;  // row leaders compact in place
-    if ((W.lane & 15) == 0 && mine) W.rl[(uint32_t)W.row * W.rcap + nr] = e;
-    nr += mine;
-    n0 += rb & 1u;
-    n1 += (rb >> 1) & 1u;
-    n2 += (rb >> 2) & 1u;
-    n3 += (rb >> 3) & 1u;
-  }
-  W.len0 = n0;
-  W.len1 = n1;
-  W.len2 = n2;
-  W.len3 = n3;
-  W.rlen = nr;
-  W.done = 0;
-  LSK_PT(tp0);
-  process_steps<MODE>(s, W, A, 0, max_len(W));
-  LSK_PADD(W.prof[MODE], tp0);
-  W.done = max_len(W);
 }
 
 __device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
@@ -695,7 +710,11 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
   W.seed = A.seed;
   W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
   W.done = 0;
-  W.list_ok = true;
+  uint32_t logq[kLogWords], logm[kLogWords];  // private (scratch) pass-1 log
+  W.logq = logq;
+  W.logm = logm;
+  W.logn = 0;
+  W.logging = W.log_ok = false;
   W.guard = 0;
 #ifdef LSK_PROFILE
   for (int i = 0; i < 8; i++) W.prof[i] = 0;
@@ -786,17 +805,16 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
       }
 #pragma unroll 8
       for (int j = 0; j < kPool / lsk::kWave; j++) W.L->pool[j * lsk::kWave + lane] = 0u;
-      if (first || !W.list_ok) {
-        if (!first) W.list_ok = false;  // lists rebuilt as work queues only
-        LSK_PT(tt0);
-        traverse<MODE_HIST>(s, W, A);
-        LSK_PADD(W.prof[2], tt0);
-        if (!first) W.list_ok = false;
-      } else {
-        LSK_PT(tr0);
-        replay<MODE_HIST>(s, W, A);
-        LSK_PADD(W.prof[4], tr0);
-      }
+      // pass 1 walks and logs; later passes replay the log when it is complete
+      W.logging = first;
+      if (first) W.log_ok = true;
+      LSK_PT(tt0);
+      if (!first && W.log_ok)
+        traverse<MODE_HIST, true>(s, W, A);
+      else
+        traverse<MODE_HIST, false>(s, W, A);
+      LSK_PADD(W.prof[2], tt0);
+      W.logging = false;
       first = false;
       bool ovf = false;
       if (s.state == ST_HIST) {
@@ -843,7 +861,7 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
           }
         }
       }
-      if (__ballot(ovf)) W.list_ok = false;
+      if (__ballot(ovf)) W.log_ok = false;  // the next range lies above pass 1's bound
     }
     if (limit) break;
     const uint32_t need = s.state == ST_READY ? s.bc : 0u;
@@ -865,15 +883,17 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
     }
   }
 
-  if (!W.list_ok) qs |= QS_LIST_INVALID;
+  if (!W.log_ok) qs |= QS_LIST_INVALID;
   if (!limit && __ballot(s.state == ST_READY)) {
     if (s.state != ST_READY) s.band_lo = s.band_w = 0;
     s.coff = pool_off;
     s.ccnt = 0;
     LSK_PT(tc0);
-    if (W.list_ok) replay<MODE_COLLECT>(s, W, A);
-    else traverse<MODE_COLLECT>(s, W, A);
-    LSK_PADD(W.prof[W.list_ok ? 5 : 3], tc0);
+    if (W.log_ok)
+      traverse<MODE_COLLECT, true>(s, W, A);
+    else
+      traverse<MODE_COLLECT, false>(s, W, A);
+    LSK_PADD(W.prof[3], tc0);
     LSK_PT(ts0);
     if (s.state == ST_READY) {
       qs |= QS_COLLECTED;
@@ -929,7 +949,7 @@ __global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const
       atomicAdd(&A.stats[6], c_ref);
       atomicAdd(&A.stats[7], c_mm);
       atomicAdd(&A.stats[8], (unsigned long long)limit);
-      atomicAdd(&A.stats[9], W.list_ok ? 0ull : 1ull);
+      atomicAdd(&A.stats[9], W.log_ok ? 0ull : 1ull);
       atomicAdd(&A.stats[10], 1ull);
       atomicAdd(&A.stats[11], c_hint);
       atomicAdd(&A.stats[12], (unsigned long long)W.steps);
@@ -961,16 +981,13 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
   const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
-  // Row-list capacity: 32 entries per row keeps the block at 26 KB of LDS (5 waves/SIMD);
-  // the lists are per-pass work queues. 256 also replays them across passes but costs
-  // occupancy (measured slower). LSK_ROWS_RCAP=64/256 select other instances (tuning).
+  // Row work-queue capacity 32 entries per row: 26 KB of LDS per 4-wave block, 6 blocks
+  // per CU. LSK_ROWS_RCAP=64 selects the larger-queue instance (tuning experiments).
   static const int rcap = [] {
     const char *e = getenv("LSK_ROWS_RCAP");
     return e ? atoi(e) : 32;
   }();
-  if (rcap == 256)
-    knn_rows_kernel<256><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
-  else if (rcap == 64)
+  if (rcap == 64)
     knn_rows_kernel<64><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   else
     knn_rows_kernel<32><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
