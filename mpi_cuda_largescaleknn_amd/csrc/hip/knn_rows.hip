@@ -562,6 +562,16 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
                                           : (s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f);
       if (lvl + 2 <= depth - 1) {
         const uint32_t g0 = 4u * node;
+        // visiting order: by bucket-index gap between the child's subtree and the wave's
+        // own bucket (tree 0; scalar integer ops) — Morton order makes that a cheap proxy
+        // for spatial distance; other trees keep index order
+        const uint32_t csh = (uint32_t)(depth - lvl - 2);
+        auto korder = [&](uint32_t ch, uint32_t j) -> uint32_t {
+          if (t != 0) return 3u - j;
+          const uint32_t b0 = (ch - (1u << (lvl + 2))) << csh, b1 = b0 + (1u << csh);
+          const uint32_t gap = W.g < b0 ? b0 - W.g : (W.g >= b1 ? W.g - b1 + 1u : 0u);
+          return (min(gap, 0x3fffffffu) << 2) | j;
+        };
         // test the 4 grandchildren; key = (center distance bits & ~3) | index, so the
         // nearest is pushed last (popped first); scalar variables only (no arrays: an
         // array here ends up in scratch and makes the stack index divergent)
@@ -570,25 +580,25 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
           const lsk::v4f lo = nodes[2 * g0], hi = nodes[2 * g0 + 1];
           const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
           need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 1u : 0u;
-          k0 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 0u;
+          k0 = korder(g0 + 0u, 0u);
         }
         {
           const lsk::v4f lo = nodes[2 * g0 + 2], hi = nodes[2 * g0 + 3];
           const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
           need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 2u : 0u;
-          k1 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 1u;
+          k1 = korder(g0 + 1u, 1u);
         }
         {
           const lsk::v4f lo = nodes[2 * g0 + 4], hi = nodes[2 * g0 + 5];
           const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
           need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 4u : 0u;
-          k2 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 2u;
+          k2 = korder(g0 + 2u, 2u);
         }
         {
           const lsk::v4f lo = nodes[2 * g0 + 6], hi = nodes[2 * g0 + 7];
           const lsk::vec3f bl{lo.x, lo.y, lo.z}, bh{hi.x, hi.y, hi.z};
           need |= __ballot(lsk::box_dist2(q, bl, bh) < lim) != 0 ? 8u : 0u;
-          k3 = (ubits(lsk::box_dist2(c, bl, bh)) & ~3u) | 3u;
+          k3 = korder(g0 + 3u, 3u);
         }
         need = (uint32_t)__builtin_amdgcn_readfirstlane((int)need);
         // sorting network, descending (push far ... near)
@@ -610,9 +620,9 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         const lsk::v4f l1 = nodes[2 * c1], h1 = nodes[2 * c1 + 1];
         const bool n0 = __ballot(lsk::box_dist2(q, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z}) < lim) != 0;
         const bool n1 = __ballot(lsk::box_dist2(q, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z}) < lim) != 0;
-        const float e0 = lsk::box_dist2(c, {l0.x, l0.y, l0.z}, {h0.x, h0.y, h0.z});
-        const float e1 = lsk::box_dist2(c, {l1.x, l1.y, l1.z}, {h1.x, h1.y, h1.z});
-        const bool first0 = ubits(e0) <= ubits(e1);  // uniform
+        // near child first: the one whose buckets contain / precede the wave's bucket
+        const uint32_t mid = ((c1 - (1u << (lvl + 1))) << (uint32_t)(depth - lvl - 1));
+        const bool first0 = t != 0 || W.g < mid;
         const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
         const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
         if (na) stk = W.lane == (int)sp++ ? a : stk;
@@ -684,7 +694,7 @@ enum : uint32_t {
 };
 
 template <int RCAP>
-__global__ __launch_bounds__(kThreads, LSK_ROWS_MINW) void knn_rows_kernel(const lsk_knn_args A) {
+__global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_rows_kernel(const lsk_knn_args A) {
   __shared__ WaveLdsR<RCAP> lds[kWavesPerBlock];
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
