@@ -71,6 +71,7 @@ class KnnArgs(C.Structure):
         ("qstatus", vp),
         ("seed", C.c_int32),
         ("pad0", C.c_int32),
+        ("init_d2", vp),
     ]
 
 
@@ -136,6 +137,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),
         "lsk_hip_flag_query_groups": ([vp, vp, i64, vp, C.c_int32, i64, vp, vp], i32),
+        "lsk_hip_flag_groups_inverse": ([vp, i64, vp, C.c_int32, i64, vp, vp], i32),
         "lsk_hip_compact_flags": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_halo_pack": ([vp, vp, i64, i32, vp, vp, vp, vp], i32),
         "lsk_hip_mask_counts": ([vp, i64, i32, vp, vp], i32),

@@ -112,6 +112,50 @@ __global__ __launch_bounds__(256) void flag_groups_kernel(const float *__restric
   if (lane == 0) flags[g] = flagged ? 1u : 0u;
 }
 
+// Inverse flagging: one lane per halo point walks the LOCAL tree, whose node boxes carry
+// the max k-th squared radius of their queries (lo.w, set by tree_set_radii), and marks
+// every bucket (= query group) whose radius-inflated box contains the point. A group can
+// only change if some halo point lies within some query's radius, and box_dist2 <=
+// dist2 for every query of the bucket, so the flags are a superset of what must be
+// re-queried. Unlike testing groups against the halo tree, the outcome does not depend
+// on the halo tree's boxes (halo points form thin slabs, whose Morton buckets often span
+// Z-order jumps and have huge boxes).
+__global__ __launch_bounds__(256) void flag_groups_inverse_kernel(const float *__restrict__ hpts,
+                                                                  int64_t nh,
+                                                                  const float *__restrict__ lnodes,
+                                                                  int32_t depth, int64_t ngroups,
+                                                                  uint32_t *__restrict__ flags) {
+  __shared__ uint32_t stack[4][kStack];
+  const int wid = threadIdx.x >> 6, lane = lsk::lane_id();
+  const int64_t i = ((int64_t)lsk::xcd_remap(blockIdx.x, gridDim.x) * 4 + wid) * 64 + lane;
+  if (__ballot(i < nh) == 0) return;
+  const bool valid = i < nh;
+  const lsk::vec3f p = valid ? lsk::vec3f{hpts[3 * i], hpts[3 * i + 1], hpts[3 * i + 2]}
+                             : lsk::vec3f{__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  const uint32_t leaf0 = 1u << depth;
+  uint32_t sp = 0;
+  if (lane == 0) stack[wid][0] = 1u;
+  sp = 1;
+  while (sp > 0) {
+    sp--;
+    const uint32_t node = lsk::uniform(stack[wid][sp]);
+    const float *nd = lnodes + 8 * (size_t)node;
+    const bool need = valid && pub_need(p, nd);
+    if (!__ballot(need)) continue;
+    if (node >= leaf0) {
+      const int64_t b = (int64_t)(node - leaf0);
+      if (need && b < ngroups) flags[b] = 1u;
+      continue;
+    }
+    if (sp + 2 > kStack) break;  // cannot happen for depth < 32
+    if (lane == 0) {
+      stack[wid][sp] = 2 * node + 1;
+      stack[wid][sp + 1] = 2 * node;
+    }
+    sp += 2;
+  }
+}
+
 __global__ __launch_bounds__(256) void compact_kernel(const uint32_t *__restrict__ flags,
                                                       int64_t n, uint32_t *__restrict__ list,
                                                       uint32_t *__restrict__ count) {
@@ -194,6 +238,20 @@ extern "C" int lsk_hip_flag_query_groups(const float *qpts, const float *qd2, in
   flag_groups_kernel<<<lsk_blocks(ng, 4), 256, 0, (hipStream_t)stream>>>(
       qpts, qd2, nq, halo_nodes, halo_depth, nhalo, flags);
   LSK_CHECK_LAUNCH("flag_groups");
+  return 0;
+}
+
+extern "C" int lsk_hip_flag_groups_inverse(const float *halo_pts, int64_t nh,
+                                           const float *local_nodes, int32_t depth,
+                                           int64_t ngroups, uint32_t *flags, void *stream) {
+  if (nh <= 0 || ngroups <= 0) return 0;
+  if (depth < 0 || depth > 30) {
+    lsk::set_last_error("flag_groups_inverse: bad tree depth");
+    return 1;
+  }
+  flag_groups_inverse_kernel<<<lsk_blocks(nh, 256), 256, 0, (hipStream_t)stream>>>(
+      halo_pts, nh, local_nodes, depth, ngroups, flags);
+  LSK_CHECK_LAUNCH("flag_groups_inverse");
   return 0;
 }
 

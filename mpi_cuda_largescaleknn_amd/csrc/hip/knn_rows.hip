@@ -784,10 +784,18 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     qs |= QS_DONE_CUT;
   } else {
     s.state = ST_HIST;
-    const uint32_t est_b = fbits(r_est2);
-    const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;  // range top kTopBins/8 octaves above
-    const uint32_t lo0 = est_b > off ? est_b - off : 0u;
-    set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
+    const float ub = A.init_d2 ? A.init_d2[qi] : -1.f;
+    if (ub >= 0.f && ub < inf) {
+      // known upper bound (re-query): range ends just above it, no overflow possible
+      const uint32_t top_b = fbits(ub) + 1u;
+      const uint32_t span = (uint32_t)kBins << kShift0;
+      set_range(s, top_b > span ? top_b - span : 0u, kShift0, min(top_b, s.cut_lim), kUnknown);
+    } else {
+      const uint32_t est_b = fbits(r_est2);
+      const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;  // top kTopBins/8 oct. above
+      const uint32_t lo0 = est_b > off ? est_b - off : 0u;
+      set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
+    }
   }
 
   uint32_t pool_off = 0;

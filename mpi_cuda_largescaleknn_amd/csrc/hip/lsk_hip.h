@@ -95,6 +95,9 @@ typedef struct lsk_knn_args {
   int32_t seed;             // queries are tree[0]'s points: seed pass 1 with buckets
                             // [g-seed, g+seed] of tree 0 (0 = off)
   int32_t pad0;
+  const float *init_d2;     // optional [nq] known upper bound of each query's k-th squared
+                            // distance (a re-query after a halo exchange passes the local
+                            // result): the first range ends just above it (NULL = estimate)
 } lsk_knn_args;
 
 int lsk_hip_knn(const lsk_knn_args *args, void *stream);       // 64-query group kernel
@@ -114,6 +117,11 @@ int lsk_hip_flag_query_groups(const float *qpts, const float *qd2, int64_t nq,
                               const float *halo_nodes, int32_t halo_depth, int64_t nhalo,
                               uint32_t *flags, void *stream);
 // Compacts indices i with flags[i] != 0 into list; *count (device) receives the count.
+// Same purpose, exact-superset and independent of the halo tree's boxes: every halo
+// point walks the local radius-annotated tree (tree_set_radii) and sets flags[g] = 1 for
+// each bucket g whose inflated box contains it. flags must be zeroed by the caller.
+int lsk_hip_flag_groups_inverse(const float *halo_pts, int64_t nh, const float *local_nodes,
+                                int32_t depth, int64_t ngroups, uint32_t *flags, void *stream);
 int lsk_hip_compact_flags(const uint32_t *flags, int64_t n, uint32_t *list, uint32_t *count,
                           void *stream);
 // For each destination rank j: writes the points with mask bit j into send buffer at

@@ -37,7 +37,7 @@ KNN_IMPL = "rows"  # "rows" (4 x 16-query rows, quarter culling) or "wave" (64-q
 class KnnConfig:
     k: int
     max_radius: float = math.inf
-    publish_levels: int = 12       # top tree levels published for halo filtering
+    publish_levels: int = 15       # top tree levels published for halo filtering (~1K pts/box)
     collect_stats: bool = False
 
     @property
@@ -113,7 +113,8 @@ def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:
 
 def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalIndex | None = None,
           groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
-          stats: KnnStats | None = None, qstatus: torch.Tensor | None = None) -> torch.Tensor:
+          stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
+          init_d2: torch.Tensor | None = None) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
     `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order."""
     n = index.n
@@ -125,7 +126,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalInd
         trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
         raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
         K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
-                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL)
+                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL, init_d2=init_d2)
         if stats is not None:
             stats.add(raw)
         return out

@@ -203,12 +203,14 @@ def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torc
 def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hint2: float,
             out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
-            seed: int = 0, impl: str = "rows") -> torch.Tensor:
+            seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None) -> torch.Tensor:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (4 x 16-query
     rows with per-row quarter culling, default) or "wave" (64-query groups). seed > 0 declares that the
     queries are trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
+    init_d2 (optional, [nq]): a known upper bound of every query's k-th squared distance
+    (e.g. the local result before a halo re-query) that places the first range.
     """
     a = KnnArgs()
     a.qpts = _ptr(qpts)
@@ -225,6 +227,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     a.stats = _ptr(stats)
     a.qstatus = _ptr(qstatus)
     a.seed = seed
+    a.init_d2 = _ptr(init_d2)
     lib = _native.hip()
     fn = lib.lsk_hip_knn_rows if impl == "rows" else lib.lsk_hip_knn
     check(fn(C.byref(a), _stream(qpts)), "knn")

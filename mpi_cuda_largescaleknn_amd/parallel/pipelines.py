@@ -83,15 +83,38 @@ def global_box(points: torch.Tensor, comm: Comm) -> torch.Tensor:
     return box
 
 
+SPLIT_TOL = 0.02  # accepted load imbalance per rank when snapping splitters to coarse cells
+
+
 def _splitters(hist: torch.Tensor, total: int, size: int) -> list[int]:
-    """Bin starts of ranks 1..P-1 so that each rank owns ~total/P points."""
+    """Bin starts of ranks 1..P-1 so that each rank owns ~total/P points.
+
+    Each splitter is snapped to the coarsest Morton cell boundary (level m: 8^m cells,
+    2^(SPLIT_BITS-3m) histogram bins) whose count stays within SPLIT_TOL of the ideal
+    share. A rank range ending mid-cell owns a sliver of a distant cell; bucket-tree
+    nodes spanning that Z-order jump have huge boxes and blow up the halo (uniform data,
+    8 ranks: exact octants instead of octants + slivers, ~3x smaller halos)."""
     cum = torch.cumsum(hist.to(torch.int64), 0)
-    excl = torch.cat([torch.zeros(1, dtype=torch.int64), cum[:-1]])
+    excl_t = torch.cat([torch.zeros(1, dtype=torch.int64), cum])  # excl[b] = count below bin b
+    nb = hist.shape[0]
+    tol = max(1, int(SPLIT_TOL * total / max(size, 1)))
+    targets = torch.tensor([(total * j) // size for j in range(1, size)], dtype=torch.int64)
+    firsts = torch.searchsorted(excl_t[:-1], targets, right=False).tolist()
+    excl = excl_t.tolist()
     out = []
     for j in range(1, size):
         target = (total * j) // size
-        b = int(torch.searchsorted(excl, torch.tensor([target], dtype=torch.int64), right=False)[0])
-        out.append(min(max(b, out[-1] if out else 0), hist.shape[0]))
+        b = int(firsts[j - 1])
+        best = b
+        for m in range(1, SPLIT_BITS // 3 + 1):
+            step = 1 << (SPLIT_BITS - 3 * m)
+            lo = (b // step) * step
+            cands = [c for c in (lo, min(lo + step, nb)) if 0 <= c <= nb]
+            c = min(cands, key=lambda x: abs(excl[x] - target))
+            if abs(excl[c] - target) <= tol:
+                best = c
+                break
+        out.append(min(max(best, out[-1] if out else 0), nb))
     return out
 
 
@@ -209,9 +232,10 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
         from .. import _native
         lib = _native.hip()
         ng = (n + 63) // 64
-        flags = torch.empty(ng, dtype=torch.int32, device=dev)
-        K.check(lib.lsk_hip_flag_query_groups(index.pts.data_ptr(), d2.data_ptr(), n, hidx.nodes.data_ptr(),
-                                              hidx.depth, nh, flags.data_ptr(), K._stream(pts)), "flag_groups")
+        flags = torch.zeros(ng, dtype=torch.int32, device=dev)
+        # halo points against the local radius-annotated tree (tree_set_radii above)
+        K.check(lib.lsk_hip_flag_groups_inverse(hidx.pts.data_ptr(), nh, index.nodes.data_ptr(), index.depth,
+                                                ng, flags.data_ptr(), K._stream(pts)), "flag_groups")
         glist = torch.empty(ng, dtype=torch.int32, device=dev)
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         K.check(lib.lsk_hip_compact_flags(flags.data_ptr(), ng, glist.data_ptr(), cnt.data_ptr(),
@@ -220,8 +244,10 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
         info.counts["requery_groups"] = nflag
         info.timer.mark("halo_tree")
         if nflag:
+            # the local k-th distance bounds the true one from above: the re-query starts
+            # with a tight first range
             E.query(index, cfg, hint2, extra=hidx, groups=glist, ngroups=nflag, out=d2,
-                    stats=info.stats if cfg.collect_stats else None)
+                    stats=info.stats if cfg.collect_stats else None, init_d2=d2)
     else:
         info.timer.mark("halo_tree")
         E.query(index, cfg, hint2, extra=hidx, out=d2)

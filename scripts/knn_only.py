@@ -13,11 +13,14 @@ ap.add_argument("--points", type=float, default=1e8)
 ap.add_argument("--k", type=int, default=100)
 ap.add_argument("--reps", type=int, default=1)
 ap.add_argument("--impl", default="rows")
+ap.add_argument("--seed", type=int, default=None)
 a = ap.parse_args()
 n = int(a.points)
 g = torch.Generator(device="cuda").manual_seed(1)
 p = torch.rand((n, 3), generator=g, device="cuda")
 E.KNN_IMPL = a.impl
+if a.seed is not None:
+    E.SEED_BUCKETS = a.seed
 idx = E.build_index(p)
 cfg = E.KnnConfig(k=a.k)
 hint2 = E.radius_hint2(idx.box, n, a.k)
