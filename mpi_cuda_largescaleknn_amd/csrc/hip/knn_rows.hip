@@ -233,6 +233,8 @@ struct WaveCtx {
   uint32_t logn;
   bool logging, log_ok;
   uint32_t *logq, *logm;
+  const float *p0, *p1, *pdef;  // tree point arrays (pdef: one that is non-empty)
+  uint32_t n0, n1;
   uint32_t guard;  // watchdog trips of the walk (never expected; see traverse)
 #ifdef LSK_PROFILE
   uint64_t prof[8];
@@ -254,22 +256,21 @@ __device__ __forceinline__ lsk_tree_view pick_tree(const lsk_knn_args &A, uint32
 // Entry = (tree << 31) | quarter id. Loads this lane's candidate of its row's quarter.
 // Branch-free (the load is always issued, from a clamped in-bounds address), so the
 // compiler can count outstanding loads and the prefetch is not serialised by vmcnt(0).
-__device__ __forceinline__ uint32_t load_quarter(const lsk_knn_args &A, uint32_t e, int lane,
-                                                 float &px, float &py, float &pz) {
+// 32-bit index math (trees hold < 2^31 points, checked on the host).
+__device__ __forceinline__ uint32_t load_quarter(const WaveCtx &W, uint32_t e, float &px, float &py,
+                                                 float &pz) {
   const bool ok = e != kInvalid;
-  // invalid entries read point 0 of a non-empty tree (lists only exist when one is)
-  const bool t1 = ok ? (e >> 31) != 0 : A.tree[0].n <= 0;
-  const float *pts = t1 ? A.tree[1].pts : A.tree[0].pts;
-  const int64_t n = t1 ? A.tree[1].n : A.tree[0].n;
-  const int64_t base = ok ? (int64_t)(e & 0x7fffffffu) * 16 : 0;
-  const int64_t rem = ok ? n - base : 0;
-  const int64_t j = (int64_t)(lane & 15);
-  const bool live = j < rem;
-  const float *p = pts + 3 * (live ? base + j : 0);
+  const bool t1 = (e >> 31) != 0;
+  const uint32_t n = t1 ? W.n1 : W.n0;
+  const uint32_t q16 = (e & 0x7fffffffu) << 4;
+  const uint32_t idx = q16 | (uint32_t)(W.lane & 15);
+  const bool live = ok && idx < n;
+  // dead lanes read point 0 of a non-empty tree
+  const float *p = live ? (t1 ? W.p1 : W.p0) + 3u * idx : W.pdef;
   px = p[0];  // raw: the consumer substitutes +inf for padding lanes (see process_steps)
   py = p[1];
   pz = p[2];
-  return rem < 16 ? (uint32_t)rem : 16u;
+  return ok ? min(n - q16, 16u) : 0u;
 }
 
 __device__ __forceinline__ uint32_t row_entry(const WaveCtx &W, uint32_t step) {
@@ -288,13 +289,13 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
   // the compiler's count of outstanding loads
   const uint32_t last = e - 1;
   float px, py, pz;
-  uint32_t cnt = load_quarter(A, row_entry(W, b), W.lane, px, py, pz);
+  uint32_t cnt = load_quarter(W, row_entry(W, b), px, py, pz);
   const float inf = __builtin_inff();
   for (uint32_t st = b; st < e; st++) {
     const uint32_t ccnt = cnt;
     const bool live = (uint32_t)(W.lane & 15) < ccnt;
     const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
-    cnt = load_quarter(A, row_entry(W, min(st + 1, last)), W.lane, px, py, pz);
+    cnt = load_quarter(W, row_entry(W, min(st + 1, last)), px, py, pz);
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
     process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
@@ -725,6 +726,11 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   W.logm = logm;
   W.logn = 0;
   W.logging = W.log_ok = false;
+  W.p0 = A.tree[0].pts;
+  W.p1 = A.ntrees > 1 ? A.tree[1].pts : A.tree[0].pts;
+  W.n0 = A.ntrees > 0 ? (uint32_t)A.tree[0].n : 0u;
+  W.n1 = A.ntrees > 1 ? (uint32_t)A.tree[1].n : 0u;
+  W.pdef = W.n0 > 0 ? W.p0 : W.p1;
   W.guard = 0;
 #ifdef LSK_PROFILE
   for (int i = 0; i < 8; i++) W.prof[i] = 0;
