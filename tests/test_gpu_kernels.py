@@ -180,3 +180,17 @@ def test_repeat_runs_and_kernels_bitwise_identical(monkeypatch):
         monkeypatch.setattr(E, "KNN_IMPL", impl)
         outs.append(E.knn_distances(p, 32).cpu())
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("scale", [1.0, 1.5, 64.0])
+def test_knn_known_upper_bound_init(scale):
+    """A re-query seeded with a known upper bound of each k-th distance (init_d2) gives
+    the same bits, whether the bound is exact, loose, or very loose."""
+    p = GENERATORS["clustered"](40000, seed=21)
+    idx = E.build_index(p.to(DEV))
+    cfg = E.KnnConfig(k=50)
+    hint2 = E.radius_hint2(idx.box, p.shape[0], 50)
+    ref = E.query(idx, cfg, hint2).clone()
+    init = ref * scale
+    got = E.query(idx, cfg, hint2, init_d2=init)
+    assert torch.equal(got.cpu(), ref.cpu())
