@@ -99,7 +99,7 @@ def _declare_host(lib: C.CDLL) -> None:
         f.restype = None
     lib.lsk_cpu_bounds.argtypes = [vp, i64, vp, i32]
     lib.lsk_cpu_bounds.restype = None
-    lib.lsk_cpu_morton.argtypes = [vp, i64, vp, C.c_float, vp, i32]
+    lib.lsk_cpu_morton.argtypes = [vp, i64, vp, C.c_float, vp, i32, i32]
     lib.lsk_cpu_morton.restype = None
     lib.lsk_cpu_halo_mask.argtypes = [vp, i64, vp, vp, i32, i32, vp, i32]
     lib.lsk_cpu_halo_mask.restype = None
@@ -120,7 +120,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_bounds_ws_bytes": ([i64], C.c_size_t),
         "lsk_hip_bounds": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_box_finalize": ([vp, vp], i32),
-        "lsk_hip_morton": ([vp, i64, vp, vp, vp, vp], i32),
+        "lsk_hip_morton": ([vp, i64, vp, vp, vp, i32, vp], i32),
         "lsk_hip_gather3": ([vp, vp, i64, vp, vp], i32),
         "lsk_hip_scatter1": ([vp, vp, i64, vp, i32, vp], i32),
         "lsk_hip_finalize": ([vp, i64, vp, vp], i32),

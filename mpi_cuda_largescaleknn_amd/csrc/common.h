@@ -84,6 +84,49 @@ LSK_HD uint32_t morton3(uint32_t ix, uint32_t iy, uint32_t iz) {
   return (morton_spread10(ix) << 2) | (morton_spread10(iy) << 1) | morton_spread10(iz);
 }
 
+// --- Hilbert keys: 10 bits per axis, 30-bit key ------------------------------------
+// Skilling's transform (axes -> transposed Hilbert index, then bit interleave). Like
+// Morton, every aligned block of 8^l consecutive keys is one octree cell of level 10-l
+// (what the splitter snapping relies on), but consecutive cells are always face
+// neighbours: 16-point runs have ~3x smaller boxes than Z-order runs (uniform data:
+// mean box volume 1.1x vs 3.3x the ideal cube), so rows and buckets cull much better.
+LSK_HD uint32_t hilbert3(uint32_t x, uint32_t y, uint32_t z) {
+  x &= 0x3ffu;
+  y &= 0x3ffu;
+  z &= 0x3ffu;
+  for (uint32_t q = 1u << 9; q > 1u; q >>= 1) {
+    const uint32_t p = q - 1u;
+    // axis 0: invert low bits of x when its bit is set (exchange with itself = no-op)
+    if (x & q) x ^= p;
+    if (y & q) {
+      x ^= p;
+    } else {
+      const uint32_t t = (x ^ y) & p;
+      x ^= t;
+      y ^= t;
+    }
+    if (z & q) {
+      x ^= p;
+    } else {
+      const uint32_t t = (x ^ z) & p;
+      x ^= t;
+      z ^= t;
+    }
+  }
+  y ^= x;  // Gray encode
+  z ^= y;
+  uint32_t t = 0;
+  for (uint32_t q = 1u << 9; q > 1u; q >>= 1)
+    if (z & q) t ^= q - 1u;
+  return morton3(x ^ t, y ^ t, z ^ t);
+}
+
+enum : int { kCurveMorton = 0, kCurveHilbert = 1 };
+
+LSK_HD uint32_t curve3(int curve, uint32_t ix, uint32_t iy, uint32_t iz) {
+  return curve == kCurveHilbert ? hilbert3(ix, iy, iz) : morton3(ix, iy, iz);
+}
+
 // --- float <-> ordered bits (non-negative floats order like their bit patterns) ---
 LSK_HD uint32_t fbits(float f) {
   union { float f; uint32_t u; } c; c.f = f; return c.u;

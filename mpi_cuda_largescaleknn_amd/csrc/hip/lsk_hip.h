@@ -32,9 +32,10 @@ size_t lsk_hip_bounds_ws_bytes(int64_t n);
 int lsk_hip_bounds(const float *pts, int64_t n, float *box_out, void *ws, void *stream);
 // Recompute box_out[6..7] from box_out[0..5] (after a cross-rank min/max reduction).
 int lsk_hip_box_finalize(float *box, void *stream);
-// keys[i] = Morton30(pts[i]) in the cube of `box`; vals[i] = i.
+// keys[i] = 30-bit space-filling-curve key of pts[i] in the cube of `box` (curve:
+// 0 = Morton, 1 = Hilbert, common.h); vals[i] = i (if vals is not null).
 int lsk_hip_morton(const float *pts, int64_t n, const float *box, uint32_t *keys,
-                   uint32_t *vals, void *stream);
+                   uint32_t *vals, int curve, void *stream);
 // dst[i] = src[idx[i]] (float3 gather).
 int lsk_hip_gather3(const float *src, const uint32_t *idx, int64_t n, float *dst, void *stream);
 // dst[idx[i]] = src[i] (float scatter), optional sqrt-finalisation.

@@ -98,14 +98,14 @@ __global__ void box_finalize_kernel(float *box) {
 __global__ __launch_bounds__(256) void morton_kernel(const float *__restrict__ pts, int64_t n,
                                                      const float *__restrict__ box,
                                                      uint32_t *__restrict__ keys,
-                                                     uint32_t *__restrict__ vals) {
+                                                     uint32_t *__restrict__ vals, int curve) {
   const float ox = box[0], oy = box[1], oz = box[2], s = box[6];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t ix = lsk::morton_quant(pts[3 * i], ox, s);
     const uint32_t iy = lsk::morton_quant(pts[3 * i + 1], oy, s);
     const uint32_t iz = lsk::morton_quant(pts[3 * i + 2], oz, s);
-    keys[i] = lsk::morton3(ix, iy, iz);
+    keys[i] = lsk::curve3(curve, ix, iy, iz);
     if (vals) vals[i] = (uint32_t)i;
   }
 }
@@ -205,10 +205,10 @@ extern "C" int lsk_hip_box_finalize(float *box, void *stream) {
 }
 
 extern "C" int lsk_hip_morton(const float *pts, int64_t n, const float *box, uint32_t *keys,
-                              uint32_t *vals, void *stream) {
+                              uint32_t *vals, int curve, void *stream) {
   if (n <= 0) return 0;
   morton_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(pts, n, box,
-                                                                             keys, vals);
+                                                                             keys, vals, curve);
   LSK_CHECK_LAUNCH("morton");
   return 0;
 }

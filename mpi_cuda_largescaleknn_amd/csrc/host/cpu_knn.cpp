@@ -211,13 +211,13 @@ extern "C" void lsk_cpu_bounds(const float *pts, int64_t n, float *box, int nthr
 }
 
 extern "C" void lsk_cpu_morton(const float *pts, int64_t n, const float *origin, float scale,
-                               uint32_t *keys, int nthreads) {
+                               uint32_t *keys, int curve, int nthreads) {
   parallel_for(n, nthreads, [&](int64_t b, int64_t e) {
     for (int64_t i = b; i < e; i++) {
       uint32_t ix = lsk::morton_quant(pts[3 * i + 0], origin[0], scale);
       uint32_t iy = lsk::morton_quant(pts[3 * i + 1], origin[1], scale);
       uint32_t iz = lsk::morton_quant(pts[3 * i + 2], origin[2], scale);
-      keys[i] = lsk::morton3(ix, iy, iz);
+      keys[i] = lsk::curve3(curve, ix, iy, iz);
     }
   });
 }

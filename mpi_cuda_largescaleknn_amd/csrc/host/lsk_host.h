@@ -80,9 +80,10 @@ void lsk_cpu_kth_kdtree(const float *pts, int64_t n, const float *qry, int64_t n
 // ---------------------------------------------------------------- CPU backend ops
 // AABB of n points -> box[6]. Empty set -> (+inf,-inf).
 void lsk_cpu_bounds(const float *pts, int64_t n, float *box, int nthreads);
-// 30-bit Morton keys relative to a cube (origin, scale = 1024/extent).
+// 30-bit curve keys (curve: 0 = Morton, 1 = Hilbert) relative to a cube (origin,
+// scale = 1024/extent).
 void lsk_cpu_morton(const float *pts, int64_t n, const float *origin, float scale,
-                    uint32_t *keys, int nthreads);
+                    uint32_t *keys, int curve, int nthreads);
 // For each point, the bitmask (bit j) of target sets it must be sent to: point p goes
 // to set j iff box_dist2(p, box) < r2 for some box of set j. boxes: 8 floats each
 // (lo.xyz, r2, hi.xyz, pad); box_offsets: nsets+1 offsets. skip_set excluded (-1 none).

@@ -67,20 +67,29 @@ def box_finalize(box: torch.Tensor) -> torch.Tensor:
     return box
 
 
-# --------------------------------------------------------------------------- Morton + sort
-def morton(pts: torch.Tensor, box: torch.Tensor, with_iota: bool = True):
-    """30-bit Morton keys of pts in the cube of `box`; returns (keys, iota)."""
+# --------------------------------------------------------------------------- curve keys + sort
+CURVES = {"morton": 0, "hilbert": 1}
+# Space-filling curve of the sort keys: Hilbert runs are spatially much tighter than
+# Z-order runs (fewer tree nodes and quarters per query, smaller halos); Morton kept
+# for A/B measurements (LSKNN_CURVE=morton).
+CURVE = os.environ.get("LSKNN_CURVE", "hilbert")
+
+
+def morton(pts: torch.Tensor, box: torch.Tensor, with_iota: bool = True, curve: str | None = None):
+    """30-bit space-filling-curve keys (Hilbert by default, `CURVE`) of pts in the cube
+    of `box`; returns (keys, iota)."""
+    cid = CURVES[curve or CURVE]
     n = pts.shape[0]
     keys = torch.empty(n, dtype=torch.int32, device=pts.device)
     vals = torch.empty(n, dtype=torch.int32, device=pts.device) if with_iota else None
     if is_gpu(pts):
-        check(_native.hip().lsk_hip_morton(_ptr(pts), n, _ptr(box), _ptr(keys), _ptr(vals), _stream(pts)),
-              "morton")
+        check(_native.hip().lsk_hip_morton(_ptr(pts), n, _ptr(box), _ptr(keys), _ptr(vals), cid,
+                                           _stream(pts)), "morton")
         return keys, vals
     b = box.detach().cpu()
     origin = b[0:3].contiguous()
     _native.host().lsk_cpu_morton(_ptr(pts.contiguous()), n, _ptr(origin), C.c_float(float(b[6])),
-                                  _ptr(keys), _nthreads())
+                                  _ptr(keys), cid, _nthreads())
     if vals is not None:
         vals.copy_(torch.arange(n, dtype=torch.int32))
     return keys, vals

@@ -40,11 +40,12 @@ def test_bounds_matches_torch():
     assert box[6].item() == pytest.approx(1024.0 / ex)
 
 
-def test_morton_matches_cpu():
+@pytest.mark.parametrize("curve", ["morton", "hilbert"])
+def test_curve_keys_match_cpu(curve):
     p = uniform(50000, seed=2)
     box = K.bounds(p)
-    kc, _ = K.morton(p, box)
-    kg, iota = K.morton(p.to(DEV), box.to(DEV))
+    kc, _ = K.morton(p, box, curve=curve)
+    kg, iota = K.morton(p.to(DEV), box.to(DEV), curve=curve)
     assert torch.equal(kc, kg.cpu())
     assert torch.equal(iota.cpu(), torch.arange(50000, dtype=torch.int32))
 

@@ -200,3 +200,33 @@ def test_roctx_trace_is_safe_without_profiler():
     trace.mark("lsknn:test")
     with trace.range("lsknn:test-range"):
         pass
+
+
+# --------------------------------------------------------------------------- curve keys
+def _cell_keys(coords, curve):
+    """Curve keys of grid cells (integer coords in [0, 1024)^3) via the C++ encoder."""
+    from mpi_cuda_largescaleknn_amd.ops import kernels as K
+    pts = (coords.to(torch.float32) + 0.5) / 1024.0
+    box = torch.tensor([0, 0, 0, 1, 1, 1, 1024.0, 1.0], dtype=torch.float32)
+    keys, _ = K.morton(pts, box, with_iota=False, curve=curve)
+    return keys.to(torch.int64) & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("corner", [(0, 0, 0), (992, 0, 480), (512, 512, 512)])
+def test_hilbert_cell_block_is_a_face_connected_path(corner):
+    """A 32^3 octree cell maps to one aligned block of 32^3 consecutive Hilbert keys
+    (what splitter snapping relies on), and consecutive keys are face neighbours."""
+    r = torch.arange(32)
+    g = torch.stack(torch.meshgrid(r, r, r, indexing="ij"), -1).reshape(-1, 3) + torch.tensor(corner)
+    keys = _cell_keys(g, "hilbert")
+    order = torch.argsort(keys)
+    ks = keys[order]
+    assert int(ks[0]) % (1 << 15) == 0
+    assert torch.equal(ks - ks[0], torch.arange(1 << 15))
+    steps = (g[order][1:] - g[order][:-1]).abs().sum(1)
+    assert bool((steps == 1).all())
+
+
+def test_morton_key_bit_interleave():
+    c = torch.tensor([[1, 0, 0], [0, 1, 0], [0, 0, 1], [1023, 1023, 1023]])
+    assert _cell_keys(c, "morton").tolist() == [4, 2, 1, (1 << 30) - 1]
