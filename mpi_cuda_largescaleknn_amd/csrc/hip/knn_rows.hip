@@ -48,14 +48,20 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 // to fit 80 (5 spilled VGPRs; 0.248 vs 0.261 s, 1e8 pts, k=100)
 #define LSK_ROWS_MINW 6
 #endif
-// 48 bins of 1/8 octave of d² (kShift0), initial range 4.5 octaves below / 1.5 above the
+// 48 bins of 1/8 octave of d² (kShift0), initial range 4 octaves below / 2 above the
 // estimate: 6 KB of pool per wave -> 5 waves/SIMD (64 bins: 8 KB, 4 waves/SIMD, 15 %
 // slower; 32 bins: too many refine passes). Measured on 1e8 uniform points, k=100.
 constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
 static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
 constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
+// 16 bins (2 octaves of d²) above the estimate: with Hilbert-sorted groups fewer
+// overflow retries than 12 (1e8 uniform, k=100: 0.155 vs 0.159 s; 8: 0.179 s)
 #ifndef LSK_TOP_BINS
-#define LSK_TOP_BINS 12
+#define LSK_TOP_BINS 16
+#endif
+// per-candidate wave-uniform skip of the bin update (0.154 vs 0.159 s, same data)
+#ifndef LSK_HIST_SKIP
+#define LSK_HIST_SKIP 1
 #endif
 constexpr int kTopBins = LSK_TOP_BINS;  // bins of the initial range above the estimate
 constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(log2(kBins))
@@ -172,6 +178,11 @@ __device__ __forceinline__ void update8(Lane &s, const uint32_t (&u)[8], uint32_
     for (int t = 0; t < 8; t++) {
       const uint32_t v = u[t];
       const bool in = v < hb;
+#if LSK_HIST_SKIP
+      // most candidates lie beyond every lane's bound once the histogram has settled:
+      // skip the bin update for the whole wave (scalar branch) when none is in range
+      if (!__ballot(in)) continue;
+#endif
       const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
       uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
       if (kBins < 64) dw = min(dw, (uint32_t)(kBins / 2 - 1));  // stay inside the pool
