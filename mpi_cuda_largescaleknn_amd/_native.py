@@ -125,7 +125,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_scatter1": ([vp, vp, i64, vp, i32, vp], i32),
         "lsk_hip_finalize": ([vp, i64, vp, vp], i32),
         "lsk_hip_dest_rank": ([vp, i64, vp, i32, i32, vp, vp, vp], i32),
-        "lsk_hip_key_histogram": ([vp, i64, i32, vp, vp], i32),
+        "lsk_hip_key_histogram": ([vp, i64, i32, i32, vp, vp], i32),
         "lsk_hip_count_dest": ([vp, i64, i32, vp, vp], i32),
         "lsk_hip_sort_ws_bytes": ([i64], C.c_size_t),
         "lsk_hip_sort_pairs": ([vp, vp, vp, vp, i64, i32, vp, C.POINTER(C.c_int), vp], i32),

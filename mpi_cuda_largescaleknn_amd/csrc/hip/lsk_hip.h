@@ -46,8 +46,9 @@ int lsk_hip_finalize(const float *src, int64_t n, float *dst, void *stream);
 // keys[i] = destination rank of point i: number of splitters s with (morton>>shift) >= s.
 int lsk_hip_dest_rank(const uint32_t *morton, int64_t n, const uint32_t *splitters,
                       int nsplit, int shift, uint32_t *dest, uint32_t *vals, void *stream);
-// hist[morton >> shift] += 1 (hist: uint32 of size 1<<(30-shift), zeroed by caller).
-int lsk_hip_key_histogram(const uint32_t *keys, int64_t n, int shift, uint32_t *hist,
+// hist[key >> shift] += 1 over every `sample`-th key (hist: uint32 of size
+// 1<<(30-shift), zeroed by caller).
+int lsk_hip_key_histogram(const uint32_t *keys, int64_t n, int shift, int sample, uint32_t *hist,
                           void *stream);
 // counts[dest[i]] += 1 for dest < ndest (counts zeroed by caller).
 int lsk_hip_count_dest(const uint32_t *dest, int64_t n, int ndest, uint32_t *counts,

@@ -66,18 +66,52 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *w
   return pre + x - v;
 }
 
-__global__ __launch_bounds__(1024) void scan_kernel(uint32_t *__restrict__ counts, int64_t total) {
-  __shared__ uint32_t wave_tot[16];
+// In-place exclusive scan of the digit-major counts by one 1024-thread block, in
+// coalesced chunks of 8 consecutive counts per thread (two 16-byte loads), carrying the
+// running total between chunks. (A per-thread contiguous segment instead makes every
+// wave touch 64 cache lines per step: 0.6-0.75 ms per pass at 2048 blocks.)
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 8;
+__global__ __launch_bounds__(kScanThreads) void scan_kernel(uint32_t *__restrict__ counts,
+                                                            int64_t total) {
+  __shared__ uint32_t wave_tot[kScanThreads / 64];
+  __shared__ uint32_t carry_s;
   const int t = threadIdx.x;
-  const int64_t seg = (total + 1023) / 1024;
-  const int64_t b = t * seg, e = b + seg < total ? b + seg : total;
-  uint32_t s = 0;
-  for (int64_t i = b; i < e; i++) s += counts[i];
-  uint32_t run = block_exclusive_scan<1024>(s, wave_tot, nullptr);
-  for (int64_t i = b; i < e; i++) {
-    uint32_t c = counts[i];
-    counts[i] = run;
-    run += c;
+  if (t == 0) carry_s = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < total; base += (int64_t)kScanThreads * kScanPer) {
+    const int64_t i0 = base + (int64_t)t * kScanPer;
+    uint32_t v[kScanPer];
+    if (i0 + kScanPer <= total) {
+      const uint4 a = *(const uint4 *)(counts + i0), b = *(const uint4 *)(counts + i0 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kScanPer; j++) v[j] = i0 + j < total ? counts[i0 + j] : 0u;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanPer; j++) s += v[j];
+    uint32_t tot;
+    const uint32_t carry = carry_s;
+    uint32_t run = carry + block_exclusive_scan<kScanThreads>(s, wave_tot, &tot);
+#pragma unroll
+    for (int j = 0; j < kScanPer; j++) {
+      const uint32_t c = v[j];
+      v[j] = run;
+      run += c;
+    }
+    if (i0 + kScanPer <= total) {
+      *(uint4 *)(counts + i0) = make_uint4(v[0], v[1], v[2], v[3]);
+      *(uint4 *)(counts + i0 + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kScanPer; j++)
+        if (i0 + j < total) counts[i0 + j] = v[j];
+    }
+    if (t == 0) carry_s = carry + tot;  // every thread read carry_s before the scan's barriers
+    __syncthreads();
   }
 }
 

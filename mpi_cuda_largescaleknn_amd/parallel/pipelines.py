@@ -84,6 +84,13 @@ def global_box(points: torch.Tensor, comm: Comm) -> torch.Tensor:
 
 
 SPLIT_TOL = 0.02  # accepted load imbalance per rank when snapping splitters to coarse cells
+HIST_SAMPLE = 8   # splitter histogram over every 8th key of ranks holding >= 2^20 points
+
+
+def _hist_sample(n: int) -> int:
+    """Key sampling stride of the splitter histogram (balance only; exactness does not
+    depend on the splitters)."""
+    return HIST_SAMPLE if n >= (1 << 20) else 1
 
 
 def _splitters(hist: torch.Tensor, total: int, size: int) -> list[int]:
@@ -154,9 +161,11 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
     if K.is_gpu(keys):
         from .. import _native
         K.check(_native.hip().lsk_hip_key_histogram(keys.data_ptr(), keys.shape[0], 30 - SPLIT_BITS,
-                                                   hist.data_ptr(), K._stream(keys)), "key_histogram")
+                                                   _hist_sample(keys.shape[0]), hist.data_ptr(),
+                                                   K._stream(keys)), "key_histogram")
     else:
-        hist += torch.bincount((keys.to(torch.int64) >> (30 - SPLIT_BITS)), minlength=nb).to(torch.int32)
+        sk = keys[::_hist_sample(keys.shape[0])]
+        hist += torch.bincount((sk.to(torch.int64) >> (30 - SPLIT_BITS)), minlength=nb).to(torch.int32)
     comm.allreduce_(hist, "sum")
     hist_h = hist.cpu()
     total = int(hist_h.to(torch.int64).sum())
