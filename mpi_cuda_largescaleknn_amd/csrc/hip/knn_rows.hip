@@ -235,10 +235,13 @@ struct WaveCtx {
   uint32_t g;
   int32_t seed;
   float cx, cy, cz;
-  uint32_t len0, len1, len2, len3;  // row list lengths (wave-uniform)
-  uint32_t rlen;                    // this lane's row's length (per lane; no select chain:
-                                    // the compiler turns one into a scratch lookup table)
-  uint32_t done;                    // lockstep steps already processed
+  // Row queues are circular (RCAP entries, a power of two) with their own heads: a step
+  // consumes the head entry of every row that has one, so a row that got ahead does not
+  // force the others to idle until a reset (lockstep idle only when a row is empty).
+  uint32_t len0, len1, len2, len3;  // row queue tails = entries appended (wave-uniform)
+  uint32_t hd0, hd1, hd2, hd3;      // row queue heads = entries consumed (wave-uniform)
+  uint32_t rlen, rhead;             // this lane's row's tail / head (per lane; no select
+                                    // chain: the compiler turns one into a scratch table)
   // pass-1 log of the visited pre-leaf nodes: entry n = (first quarter | tree << 31,
   // 4 row bits per quarter) held by lane n % 64 of word n / 64 of two private arrays
   uint32_t logn;
@@ -253,11 +256,12 @@ struct WaveCtx {
   uint32_t steps, quarters, nodes_visited, csteps, cnodes;
 };
 
-__device__ __forceinline__ uint32_t max_len(const WaveCtx &W) {
-  return max(max(W.len0, W.len1), max(W.len2, W.len3));
+// pending (appended, not yet processed) entries of the longest / shortest row queue
+__device__ __forceinline__ uint32_t max_pend(const WaveCtx &W) {
+  return max(max(W.len0 - W.hd0, W.len1 - W.hd1), max(W.len2 - W.hd2, W.len3 - W.hd3));
 }
-__device__ __forceinline__ uint32_t min_len(const WaveCtx &W) {
-  return min(min(W.len0, W.len1), min(W.len2, W.len3));
+__device__ __forceinline__ uint32_t min_pend(const WaveCtx &W) {
+  return min(min(W.len0 - W.hd0, W.len1 - W.hd1), min(W.len2 - W.hd2, W.len3 - W.hd3));
 }
 
 __device__ __forceinline__ lsk_tree_view pick_tree(const lsk_knn_args &A, uint32_t t) {
@@ -284,33 +288,37 @@ __device__ __forceinline__ uint32_t load_quarter(const WaveCtx &W, uint32_t e, f
   return ok ? min(n - q16, 16u) : 0u;
 }
 
-__device__ __forceinline__ uint32_t row_entry(const WaveCtx &W, uint32_t step) {
-  const uint32_t v = W.rl[(uint32_t)W.row * W.rcap + min(step, W.rcap - 1u)];
-  return step < W.rlen ? v : kInvalid;
+// Entry number `h` of this lane's row queue (kInvalid past the tail).
+__device__ __forceinline__ uint32_t row_entry(const WaveCtx &W, uint32_t h) {
+  const uint32_t v = W.rl[(uint32_t)W.row * W.rcap + (h & (W.rcap - 1u))];
+  return h < W.rlen ? v : kInvalid;
 }
 
-// Lockstep processing of steps [b, e): row r handles its list entry `step`.
+// n lockstep steps: every row consumes its head entry (rows with an empty queue idle).
 template <int MODE>
 __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn_args &A,
-                                              uint32_t b, uint32_t e) {
-  b = lsk::uniform(b);  // wave-uniform loop (lets the compiler keep it scalar)
-  e = lsk::uniform(e);
-  if (b >= e) return;
-  // one step of prefetch; loads are unconditional (clamped step) so no branch breaks
-  // the compiler's count of outstanding loads
-  const uint32_t last = e - 1;
+                                              uint32_t n) {
+  n = lsk::uniform(n);  // wave-uniform loop (lets the compiler keep it scalar)
+  if (n == 0) return;
+  // one step of prefetch; loads are unconditional (the entry after the last step is
+  // fetched too, harmlessly) so no branch breaks the compiler's count of outstanding loads
   float px, py, pz;
-  uint32_t cnt = load_quarter(W, row_entry(W, b), px, py, pz);
+  uint32_t cnt = load_quarter(W, row_entry(W, W.rhead), px, py, pz);
   const float inf = __builtin_inff();
-  for (uint32_t st = b; st < e; st++) {
+  for (uint32_t st = 0; st < n; st++) {
     const uint32_t ccnt = cnt;
     const bool live = (uint32_t)(W.lane & 15) < ccnt;
     const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
-    cnt = load_quarter(W, row_entry(W, min(st + 1, last)), px, py, pz);
+    W.rhead += W.rhead < W.rlen ? 1u : 0u;
+    cnt = load_quarter(W, row_entry(W, W.rhead), px, py, pz);
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
     process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
   }
+  W.hd0 = min(W.hd0 + n, W.len0);
+  W.hd1 = min(W.hd1 + n, W.len1);
+  W.hd2 = min(W.hd2 + n, W.len2);
+  W.hd3 = min(W.hd3 + n, W.len3);
 }
 
 __device__ __forceinline__ float hist_bound(const Lane &s) { return bitsf(s.hi_b); }
@@ -349,7 +357,7 @@ __device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
 // writes at its row's length (one vector LDS store), the lengths stay scalar.
 __device__ __forceinline__ void rows_append(WaveCtx &W, uint32_t rowmask, uint32_t e) {
   const uint32_t mine = (rowmask >> W.row) & 1u;
-  if ((W.lane & 15) == 0 && mine) W.rl[(uint32_t)W.row * W.rcap + W.rlen] = e;
+  if ((W.lane & 15) == 0 && mine) W.rl[(uint32_t)W.row * W.rcap + (W.rlen & (W.rcap - 1u))] = e;
   W.rlen += mine;
   W.len0 += rowmask & 1u;
   W.len1 += (rowmask >> 1) & 1u;
@@ -454,7 +462,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   const lsk::vec3f q{s.qx, s.qy, s.qz};
   const lsk::vec3f c{W.cx, W.cy, W.cz};
   W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
-  W.done = 0;
+  W.hd0 = W.hd1 = W.hd2 = W.hd3 = W.rhead = 0;
   uint32_t t = 0, sp = 0;
   // DFS stack in one VGPR (lane i = entry i; < 64 entries): v_readlane to pop, a
   // lane select to push, instead of an LDS round trip per node
@@ -478,7 +486,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     // ---- fill until every row has a batch pending, a list is nearly full or the walk ends
     for (;;) {
       // room for the pending batch (8 entries per node per row) plus one more node
-      const bool room_short = max_len(W) + 8u * (P.n + 1u) > W.rcap;
+      const bool room_short = max_pend(W) + 8u * (P.n + 1u) > W.rcap;
       if (P.n && (P.n == kPend || room_short || (started && sp == 0))) {
         LSK_PT(tq0);  // the one flush site (keeps a single inlined copy)
         flush_pending<MODE>(s, W, T.qnodes, t, P, nquarters, skip_lo, skip_hi, 32u << depth);
@@ -490,7 +498,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         overflow = true;
         break;
       }
-      if (min_len(W) >= W.done + 8u) break;
+      if (min_pend(W) >= 8u) break;
       if (!started) {
         if (t >= (uint32_t)A.ntrees) {
           finished = true;
@@ -643,15 +651,13 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
       LSK_PADD(W.prof[5], tn0);
     }
     // ---- drain (single processing call site)
-    const uint32_t target = (finished || overflow) ? max_len(W) : min_len(W);
+    // fill: the steps every row can take; overflow: at least enough to make room for one
+    // more node's 8 quarters in the longest queue; end of walk: everything pending
+    const uint32_t mxp = max_pend(W), mnp = min_pend(W);
+    const uint32_t nsteps = finished ? mxp : overflow ? max(mnp, mxp + 8u - min(mxp + 8u, W.rcap)) : mnp;
     LSK_PT(tp0);
-    process_steps<MODE>(s, W, A, W.done, target);
+    process_steps<MODE>(s, W, A, nsteps);
     LSK_PADD(W.prof[MODE], tp0);
-    W.done = target;
-    if (overflow) {
-      W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
-      W.done = 0;
-    }
   }
 }
 
@@ -731,7 +737,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   W.g = g;
   W.seed = A.seed;
   W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
-  W.done = 0;
+  W.hd0 = W.hd1 = W.hd2 = W.hd3 = W.rhead = 0;
   uint32_t logq[kLogWords], logm[kLogWords];  // private (scratch) pass-1 log
   W.logq = logq;
   W.logm = logm;
