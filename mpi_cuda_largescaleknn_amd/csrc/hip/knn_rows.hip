@@ -165,12 +165,13 @@ __device__ __forceinline__ uint32_t cand(const Lane &s, float px, float py, floa
 }
 
 template <int MODE>
-__device__ __forceinline__ void update8(Lane &s, const uint32_t (&u)[8], uint32_t *pool, int lane) {
+__device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[8], uint32_t *pool, int lane) {
   uint32_t umin = u[0];
 #pragma unroll
   for (int t = 1; t < 8; t++) umin = min(umin, u[t]);
+  const bool lane_in = umin < s.hi_b;  // (profiling: this lane had a value in range)
   if (MODE == MODE_HIST) {
-    if (!__ballot(umin < s.hi_b)) return;
+    if (!__ballot(lane_in)) return false;
     // bin = sat(v - lo_b) >> shift (< 64 for every v < hi_b); bins 2j, 2j+1 share the
     // lane's dword j as two 16-bit counters
     const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
@@ -196,7 +197,7 @@ __device__ __forceinline__ void update8(Lane &s, const uint32_t (&u)[8], uint32_
     bool any = false;
 #pragma unroll
     for (int t = 0; t < 8; t++) any = any || (u[t] - bl < bw);
-    if (!__ballot(any)) return;
+    if (!__ballot(any)) return lane_in;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
       if (u[t] - bl < bw) {
@@ -205,25 +206,28 @@ __device__ __forceinline__ void update8(Lane &s, const uint32_t (&u)[8], uint32_
       }
     }
   }
+  return lane_in;
 }
 
 // The 16 candidates of this lane's row quarter (lane i of the row holds candidate i).
 template <int MODE>
-__device__ __forceinline__ void process16(Lane &s, float px, float py, float pz, uint32_t cnt,
+__device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz, uint32_t cnt,
                                           uint32_t *pool, int lane, uint32_t k) {
+  bool lane_in;
   {
     uint32_t u[8] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
                      cand<3>(s, px, py, pz), cand<4>(s, px, py, pz), cand<5>(s, px, py, pz),
                      cand<6>(s, px, py, pz), cand<7>(s, px, py, pz)};
-    update8<MODE>(s, u, pool, lane);
+    lane_in = update8<MODE>(s, u, pool, lane);
   }
   if (__ballot(cnt > 8u)) {
     uint32_t u[8] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
                      cand<11>(s, px, py, pz), cand<12>(s, px, py, pz), cand<13>(s, px, py, pz),
                      cand<14>(s, px, py, pz), cand<15>(s, px, py, pz)};
-    update8<MODE>(s, u, pool, lane);
+    lane_in = update8<MODE>(s, u, pool, lane) || lane_in;
   }
   if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) hist_shrink(s, pool, lane, k);
+  return lane_in;
 }
 
 struct WaveCtx {
@@ -252,6 +256,7 @@ struct WaveCtx {
   uint32_t guard;  // watchdog trips of the walk (never expected; see traverse)
 #ifdef LSK_PROFILE
   uint64_t prof[8];
+  uint32_t prof_rows_entry, prof_rows_in;  // pass-1 row-steps with an entry / with a value in range
 #endif
   uint32_t steps, quarters, nodes_visited, csteps, cnodes;
 };
@@ -294,6 +299,11 @@ __device__ __forceinline__ uint32_t row_entry(const WaveCtx &W, uint32_t h) {
   return h < W.rlen ? v : kInvalid;
 }
 
+__device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
+  return ((ballot & 0xffffull) ? 1u : 0u) | ((ballot & 0xffff0000ull) ? 2u : 0u) |
+         ((ballot & 0xffff00000000ull) ? 4u : 0u) | ((ballot & 0xffff000000000000ull) ? 8u : 0u);
+}
+
 // n lockstep steps: every row consumes its head entry (rows with an empty queue idle).
 template <int MODE>
 __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn_args &A,
@@ -313,7 +323,16 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     cnt = load_quarter(W, row_entry(W, W.rhead), px, py, pz);
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
+#ifdef LSK_PROFILE
+    const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+    if (MODE == MODE_HIST) {
+      const uint32_t re = row_bits(__ballot(ccnt > 0u)), ri = row_bits(__ballot(lin));
+      W.prof_rows_entry += __popc(re);
+      W.prof_rows_in += __popc(re & ri);
+    }
+#else
     process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+#endif
   }
   W.hd0 = min(W.hd0 + n, W.len0);
   W.hd1 = min(W.hd1 + n, W.len1);
@@ -348,10 +367,6 @@ __device__ __forceinline__ bool box_retained(const Lane &s, float lx, float ly, 
   return false;
 }
 
-__device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
-  return ((ballot & 0xffffull) ? 1u : 0u) | ((ballot & 0xffff0000ull) ? 2u : 0u) |
-         ((ballot & 0xffff00000000ull) ? 4u : 0u) | ((ballot & 0xffff000000000000ull) ? 8u : 0u);
-}
 
 // Append entry e to the lists of the rows in rowmask: the leader lane of each such row
 // writes at its row's length (one vector LDS store), the lengths stay scalar.
@@ -751,6 +766,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   W.guard = 0;
 #ifdef LSK_PROFILE
   for (int i = 0; i < 8; i++) W.prof[i] = 0;
+  W.prof_rows_entry = W.prof_rows_in = 0;
   LSK_PT(twave0);
 #endif
   W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
@@ -973,6 +989,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   LSK_PADD(W.prof[7], twave0);
   if (A.stats && lane == 0)
     for (int i = 0; i < 8; i++) atomicAdd(&A.stats[16 + i], (unsigned long long)W.prof[i]);
+  if (A.stats && lane == 0) {
+    atomicAdd(&A.stats[24], (unsigned long long)W.prof_rows_entry);
+    atomicAdd(&A.stats[25], (unsigned long long)W.prof_rows_in);
+  }
 #endif
   if (A.stats) {
     auto cnt = [&](uint32_t bit) {

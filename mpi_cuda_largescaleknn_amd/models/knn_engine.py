@@ -73,7 +73,8 @@ class KnnStats:
                  "hint_lanes", "recorded_leaves", "collect_steps", "collect_nodes", "guard_trips",
                  # cycle profile (LSK_PROFILE kernel builds only)
                  "prof_proc_hist", "prof_proc_collect", "prof_walk_hist", "prof_walk_collect",
-                 "prof_quarters", "prof_inner_nodes", "prof_select", "prof_wave"]
+                 "prof_quarters", "prof_inner_nodes", "prof_select", "prof_wave",
+                 "prof_rows_entry", "prof_rows_in"]
         vals = raw.cpu().tolist()
         for i, nm in enumerate(names):
             self.counters[nm] = self.counters.get(nm, 0) + int(vals[i])
