@@ -55,6 +55,9 @@ class TreeView(C.Structure):
     ]
 
 
+HIP_ABI = 2  # lsk_hip_abi_version() of a library matching the structs below
+
+
 class KnnArgs(C.Structure):
     _fields_ = [
         ("qpts", vp),
@@ -72,6 +75,8 @@ class KnnArgs(C.Structure):
         ("seed", C.c_int32),
         ("pad0", C.c_int32),
         ("init_d2", vp),
+        ("out_perm", vp),
+        ("out_final", vp),
     ]
 
 
@@ -186,6 +191,9 @@ def hip() -> C.CDLL:
                             raise
                 lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
                 _declare_hip(lib)
+                ver = lib.lsk_hip_abi_version()
+                if ver != HIP_ABI:  # the ctypes structs below must match lsk_hip.h
+                    raise NativeError(f"{path}: ABI version {ver}, expected {HIP_ABI} (rebuild)")
                 _hip_lib = lib
     return _hip_lib
 

@@ -100,6 +100,9 @@ typedef struct lsk_knn_args {
   const float *init_d2;     // optional [nq] known upper bound of each query's k-th squared
                             // distance (a re-query after a halo exchange passes the local
                             // result): the first range ends just above it (NULL = estimate)
+  const uint32_t *out_perm; // optional fused result scatter (single-rank path): when set,
+  float *out_final;         // out_final[out_perm[q]] = sqrtf(d2) (inf stays inf) is written
+                            // instead of out_d2[q] (saves the separate scatter kernel)
 } lsk_knn_args;
 
 int lsk_hip_knn(const lsk_knn_args *args, void *stream);       // 64-query group kernel

@@ -115,22 +115,28 @@ def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:
 def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalIndex | None = None,
           groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
-          init_d2: torch.Tensor | None = None) -> torch.Tensor:
+          init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
-    `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order."""
+    `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order, or —
+    with `final_out` — writes the final distances in input order (index.perm) straight
+    from the kernel (fused scatter) and returns final_out."""
     n = index.n
     if out is None:
         out = torch.empty(n, dtype=torch.float32, device=index.device)
     if n == 0:
-        return out
+        return final_out if final_out is not None else out
+    if final_out is not None and not K.is_gpu(index.pts):
+        d2 = query(index, cfg, hint2, extra, groups, ngroups, out, stats, qstatus, init_d2)
+        return K.scatter1(d2, index.perm, final_out, finalize=True)
     if K.is_gpu(index.pts):
         trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
         raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
         K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
-                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL, init_d2=init_d2)
+                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL, init_d2=init_d2,
+                  out_perm=index.perm if final_out is not None else None, out_final=final_out)
         if stats is not None:
             stats.add(raw)
-        return out
+        return final_out if final_out is not None else out
     pts = index.pts[:n]
     if extra is not None and extra.n > 0:
         pts = torch.cat([pts, extra.pts[:extra.n]])
@@ -145,6 +151,5 @@ def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,
     cfg = KnnConfig(k=k, max_radius=max_radius)
     index = build_index(points)
     hint2 = radius_hint2(index.box, index.n, k)
-    d2 = query(index, cfg, hint2, stats=stats)
     out = torch.empty(index.n, dtype=torch.float32, device=points.device)
-    return K.scatter1(d2, index.perm, out, finalize=True)
+    return query(index, cfg, hint2, stats=stats, final_out=out)

@@ -212,7 +212,8 @@ def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torc
 def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hint2: float,
             out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
-            seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None) -> torch.Tensor:
+            seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
+            out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None) -> torch.Tensor:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (4 x 16-query
@@ -220,7 +221,14 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     queries are trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
     init_d2 (optional, [nq]): a known upper bound of every query's k-th squared distance
     (e.g. the local result before a halo re-query) that places the first range.
+    out_perm / out_final (optional, fused scatter): the kernel writes
+    out_final[out_perm[q]] = final distance instead of out_d2[q] (out_d2 is then unused).
     """
+    if (out_perm is None) != (out_final is None):
+        raise ValueError("knn_gpu: out_perm and out_final go together")
+    if out_perm is not None and (out_perm.shape[0] < nq or out_perm.dtype != torch.int32
+                                 or not out_perm.is_contiguous() or out_final.dtype != torch.float32):
+        raise ValueError("knn_gpu: out_perm must be int32 [>= nq], out_final float32")
     a = KnnArgs()
     a.qpts = _ptr(qpts)
     a.nq = nq
@@ -237,6 +245,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     a.qstatus = _ptr(qstatus)
     a.seed = seed
     a.init_d2 = _ptr(init_d2)
+    a.out_perm = _ptr(out_perm)
+    a.out_final = _ptr(out_final)
     lib = _native.hip()
     fn = lib.lsk_hip_knn_rows if impl == "rows" else lib.lsk_hip_knn
     check(fn(C.byref(a), _stream(qpts)), "knn")

@@ -283,11 +283,10 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     if comm.size == 1:
         index = E.build_index(points, box)
         info.timer.mark("build")
-        d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
-        info.timer.mark("knn_local")
+        # one rank: the k-NN kernel writes the final distances in input order (fused scatter)
         out = torch.empty(n_local, dtype=torch.float32, device=points.device)
-        K.scatter1(d2, index.perm, out, finalize=True)
-        info.timer.mark("return")
+        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
+        info.timer.mark("knn_local")
         return out
     owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
     index = E.build_index(owned, box)
@@ -321,11 +320,14 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     info.timer.mark("bounds")
     index = E.build_index(points, box)
     info.timer.mark("build")
+    out = torch.empty(n_local, dtype=torch.float32, device=points.device)
+    if comm.size == 1:  # fused scatter: final distances straight from the k-NN kernel
+        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
+        info.timer.mark("knn_local")
+        return out
     d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
     info.timer.mark("knn_local")
-    if comm.size > 1:
-        d2 = halo_refine(index, d2, comm, cfg, hint2, info)
-    out = torch.empty(n_local, dtype=torch.float32, device=points.device)
+    d2 = halo_refine(index, d2, comm, cfg, hint2, info)
     K.scatter1(d2, index.perm, out, finalize=True)
     info.timer.mark("return")
     return out

@@ -24,7 +24,7 @@ def oracle(points, k, max_radius=math.inf, method="kdtree"):
 def test_native_library_is_loaded():
     from mpi_cuda_largescaleknn_amd import _native
     lib = _native.hip()
-    assert lib.lsk_hip_abi_version() == 1
+    assert lib.lsk_hip_abi_version() == 2
     import ctypes as C
     buf = C.create_string_buffer(512)
     assert lib.lsk_hip_device_info(0, buf, 512) == 0
@@ -195,3 +195,18 @@ def test_knn_known_upper_bound_init(scale):
     init = ref * scale
     got = E.query(idx, cfg, hint2, init_d2=init)
     assert torch.equal(got.cpu(), ref.cpu())
+
+
+@pytest.mark.parametrize("impl", ["rows", "wave"])
+def test_fused_scatter_equals_separate_scatter(impl, monkeypatch):
+    """The single-rank path lets the k-NN kernel write final distances in input order
+    (out_final[perm[q]]); same bits as sorted d2 + scatter1(finalize)."""
+    monkeypatch.setattr(E, "KNN_IMPL", impl)
+    p = GENERATORS["clustered"](70001, seed=5).to(DEV)
+    idx = E.build_index(p)
+    cfg = E.KnnConfig(k=24, max_radius=0.05)
+    hint2 = E.radius_hint2(idx.box, idx.n, 24)
+    d2 = E.query(idx, cfg, hint2)
+    sep = K.scatter1(d2, idx.perm, torch.empty(idx.n, device=DEV), finalize=True)
+    fused = E.query(idx, cfg, hint2, final_out=torch.full((idx.n,), -1.0, device=DEV))
+    assert torch.equal(fused.cpu(), sep.cpu())
