@@ -49,6 +49,9 @@ def parse():
                     help="halo = MI355X pipeline; ring/peer = reference algorithm (ref-algo baseline)")
     ap.add_argument("--phases", action="store_true", help="print per-phase times (adds syncs)")
     ap.add_argument("--stats", action="store_true", help="collect k-NN kernel counters")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu = rehearsal of the launch/timing contract (gloo, CPU oracle); "
+                         "never a measurement")
     return ap.parse_args()
 
 
@@ -59,7 +62,7 @@ def make_points(n_total: int, rank: int, size: int, device, variant: str) -> tor
     n = e - b
     g = torch.Generator(device=device)
     g.manual_seed(1234 + rank)
-    host = torch.empty((n, 3), dtype=torch.float32, pin_memory=True)
+    host = torch.empty((n, 3), dtype=torch.float32, pin_memory=device.type == "cuda")
     chunk = 1 << 26
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
@@ -68,8 +71,13 @@ def make_points(n_total: int, rank: int, size: int, device, variant: str) -> tor
             # spatially tiled files: rank r owns the slab [r/size, (r+1)/size) in x
             d[:, 0] = (d[:, 0] + rank) / size
         host[s:s + m].copy_(d)
-    torch.cuda.synchronize(device)
+    _sync(device)
     return host
+
+
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
 
 
 def main():
@@ -77,10 +85,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    if args.device == "cuda":
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if device.type == "cuda":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
         comm = TorchComm(device)
     else:
         comm = SingleComm(device)
@@ -88,7 +102,7 @@ def main():
     cfg = KnnConfig(k=args.k, collect_stats=args.stats)
 
     host_pts = make_points(n_total, rank, world, device, args.variant)
-    host_out = torch.empty(host_pts.shape[0], dtype=torch.float32, pin_memory=True)
+    host_out = torch.empty(host_pts.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda")
 
     info_last = None
 
@@ -109,18 +123,18 @@ def main():
         else:
             out = PL.prepartitioned_knn(pts, comm, cfg, info)
         host_out.copy_(out, non_blocking=True)
-        torch.cuda.synchronize(device)
+        _sync(device)
         info_last = info
 
     for _ in range(args.warmup):
         step()
     comm.barrier()
-    torch.cuda.synchronize(device)
+    _sync(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     comm.barrier()
-    torch.cuda.synchronize(device)
+    _sync(device)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.allreduce_(t, "max")

@@ -63,6 +63,10 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_HIST_SKIP
 #define LSK_HIST_SKIP 1
 #endif
+// exec-masked histogram update (fewer VALU per candidate than the select form)
+#ifndef LSK_HIST_EXEC
+#define LSK_HIST_EXEC 0
+#endif
 constexpr int kTopBins = LSK_TOP_BINS;  // bins of the initial range above the estimate
 constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(log2(kBins))
 constexpr uint32_t kShift0 = 20;
@@ -179,11 +183,22 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[8], uint32_
     for (int t = 0; t < 8; t++) {
       const uint32_t v = u[t];
       const bool in = v < hb;
-#if LSK_HIST_SKIP
+#if LSK_HIST_SKIP && !LSK_HIST_EXEC  // (the exec-masked form skips by s_cbranch_execz)
       // most candidates lie beyond every lane's bound once the histogram has settled:
       // skip the bin update for the whole wave (scalar branch) when none is in range
       if (!__ballot(in)) continue;
 #endif
+#if LSK_HIST_EXEC
+      // exec-masked update: lanes out of range do not issue it, so the bin index needs
+      // no clamp (v < hi_b <= lo_b + kBins << shift) and the increment no select
+      if (in) {
+        const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
+        const uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
+        const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
+        atomicAdd(&pool[dw * lsk::kWave + lane], __umul24(half, 0xffffu) + 1u);
+        s.c_hi++;
+      }
+#else
       const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
       uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
       if (kBins < 64) dw = min(dw, (uint32_t)(kBins / 2 - 1));  // stay inside the pool
@@ -191,6 +206,7 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[8], uint32_
       const uint32_t inc = in ? __umul24(half, 0xffffu) + 1u : 0u;
       atomicAdd(&pool[dw * lsk::kWave + lane], inc);
       s.c_hi += (uint32_t)in;
+#endif
     }
   } else {
     const uint32_t bl = s.band_lo, bw = s.band_w;

@@ -1,0 +1,56 @@
+"""bench.py contract rehearsal on the CPU: the multi-rank launch path the driver uses
+(torch.distributed.run, one process per rank, barrier + max-over-ranks timing, one JSON
+line from rank 0), with the gloo backend and CPU tensors instead of RCCL and GPUs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{\"metric\"")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def _env():
+    env = dict(os.environ)
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def test_bench_single_rank_cpu():
+    out = subprocess.run([sys.executable, "bench.py", "--device", "cpu", "--points", "20000", "--k", "8",
+                          "--steps", "2", "--warmup", "1"], cwd=ROOT, env=_env(), capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 1 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["value"] > 0 and rec["higher_is_better"] is True
+    assert rec["config"]["all_finite"] is True
+
+
+@pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])
+def test_bench_two_ranks_torchrun_gloo(variant):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--device", "cpu", "--points", "30000", "--k", "16", "--steps", "2", "--warmup", "1",
+           "--variant", variant]
+    out = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 2
+    assert rec["config"]["global_batch"] == 30000
+    assert rec["config"]["all_finite"] is True
+    assert rec["ms_per_step"] > 0
