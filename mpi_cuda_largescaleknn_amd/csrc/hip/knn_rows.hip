@@ -330,6 +330,8 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
   // fetched too, harmlessly) so no branch breaks the compiler's count of outstanding loads
   float px, py, pz;
   uint32_t cnt = load_quarter(W, row_entry(W, W.rhead), px, py, pz);
+  // (two steps of prefetch: 0.155 vs 0.152 s at 6 waves/SIMD with 10 spilled VGPRs,
+  // 0.166 s at 5 waves/SIMD — occupancy, not the candidate-load distance, is what counts)
   const float inf = __builtin_inff();
   for (uint32_t st = 0; st < n; st++) {
     const uint32_t ccnt = cnt;
