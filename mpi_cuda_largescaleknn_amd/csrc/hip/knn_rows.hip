@@ -29,8 +29,9 @@
 //    quartile: groups straddling a Morton discontinuity otherwise produce a few waves
 //    with absurd first-pass bounds that dominate the kernel's tail.
 //  Inner-loop cost per candidate and lane: 6 VALU for d² (DPP broadcast folded into the
-//  subtracts) + 8 VALU + 1 ds_add for the histogram (compiled with -fno-slp-vectorize:
-//  packed-math ops cannot take DPP operands). 6 waves/SIMD (80 VGPRs, 26 KB LDS/block).
+//  subtracts) + 5 VALU + 1 exec-masked ds_add for the histogram when in range (compiled
+//  with -fno-slp-vectorize: packed-math ops cannot take DPP operands). 7 waves/SIMD
+//  (72 VGPRs, 22 KB LDS/block).
 #include "dev.h"
 
 namespace {
@@ -41,16 +42,19 @@ using lsk::fbits;
 constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #ifndef LSK_ROWS_BINS
-#define LSK_ROWS_BINS 48
+#define LSK_ROWS_BINS 40
 #endif
 #ifndef LSK_ROWS_MINW
-// 6 waves/SIMD: LDS allows 6 (26 KB/block), the allocator lands at 83 VGPRs unless told
-// to fit 80 (5 spilled VGPRs; 0.248 vs 0.261 s, 1e8 pts, k=100)
-#define LSK_ROWS_MINW 6
+// 7 waves/SIMD: 40 bins keep the LDS at 22 KB/block (7 blocks/CU) and the allocator fits
+// 72 VGPRs with 4-candidate batches (its 10 spills sit in per-pass code, not in the
+// inner loops). Occupancy is what this latency-bound kernel runs on (1e8 pts, k=100):
+// 5 waves 0.166 s, 6 waves 0.149-0.152 s, 7 waves 0.147 s, 8 waves (36 bins, 24 spills)
+// 0.155 s.
+#define LSK_ROWS_MINW 7
 #endif
-// 48 bins of 1/8 octave of d² (kShift0), initial range 4 octaves below / 2 above the
-// estimate: 6 KB of pool per wave -> 5 waves/SIMD (64 bins: 8 KB, 4 waves/SIMD, 15 %
-// slower; 32 bins: too many refine passes). Measured on 1e8 uniform points, k=100.
+// 40 bins of 1/8 octave of d² (kShift0) around the estimate (48 bins: 0.150 s at 6
+// waves/SIMD; 36 bins: more refine passes, 0.153 s at 7; 32 bins: 0.225 s).
+// Measured on 1e8 uniform points, k=100.
 constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
 static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
 constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
@@ -63,9 +67,15 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_HIST_SKIP
 #define LSK_HIST_SKIP 1
 #endif
-// exec-masked histogram update (fewer VALU per candidate than the select form)
+// candidates per distance batch in the inner loop: 4 (vs 8) frees the VGPRs that let
+// the kernel run at 7 waves/SIMD (8 at 6 waves: 0.152 s, 4 at 6 waves: 0.149 s)
+#ifndef LSK_CAND_GROUP
+#define LSK_CAND_GROUP 4
+#endif
+// exec-masked histogram update: 5 VALU + ds_add per in-range candidate instead of 8
+// (same speed — the kernel is not VALU-bound — with a shorter dependency chain)
 #ifndef LSK_HIST_EXEC
-#define LSK_HIST_EXEC 0
+#define LSK_HIST_EXEC 1
 #endif
 constexpr int kTopBins = LSK_TOP_BINS;  // bins of the initial range above the estimate
 constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(log2(kBins))
@@ -168,11 +178,11 @@ __device__ __forceinline__ uint32_t cand(const Lane &s, float px, float py, floa
   return fbits(d2);
 }
 
-template <int MODE>
-__device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[8], uint32_t *pool, int lane) {
+template <int MODE, int G>
+__device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_t *pool, int lane) {
   uint32_t umin = u[0];
 #pragma unroll
-  for (int t = 1; t < 8; t++) umin = min(umin, u[t]);
+  for (int t = 1; t < G; t++) umin = min(umin, u[t]);
   const bool lane_in = umin < s.hi_b;  // (profiling: this lane had a value in range)
   if (MODE == MODE_HIST) {
     if (!__ballot(lane_in)) return false;
@@ -180,7 +190,7 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[8], uint32_
     // lane's dword j as two 16-bit counters
     const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
+    for (int t = 0; t < G; t++) {
       const uint32_t v = u[t];
       const bool in = v < hb;
 #if LSK_HIST_SKIP && !LSK_HIST_EXEC  // (the exec-masked form skips by s_cbranch_execz)
@@ -212,10 +222,10 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[8], uint32_
     const uint32_t bl = s.band_lo, bw = s.band_w;
     bool any = false;
 #pragma unroll
-    for (int t = 0; t < 8; t++) any = any || (u[t] - bl < bw);
+    for (int t = 0; t < G; t++) any = any || (u[t] - bl < bw);
     if (!__ballot(any)) return lane_in;
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
+    for (int t = 0; t < G; t++) {
       if (u[t] - bl < bw) {
         if (s.ccnt < s.bc) pool[s.coff + s.ccnt] = u[t];
         s.ccnt++;
@@ -230,18 +240,44 @@ template <int MODE>
 __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz, uint32_t cnt,
                                           uint32_t *pool, int lane, uint32_t k) {
   bool lane_in;
+#if LSK_CAND_GROUP == 4
+  // groups of 4 candidates: 4 fewer live VGPRs in the hot loop than groups of 8
+  {
+    uint32_t u[4] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
+                     cand<3>(s, px, py, pz)};
+    lane_in = update8<MODE, 4>(s, u, pool, lane);
+  }
+  {
+    uint32_t u[4] = {cand<4>(s, px, py, pz), cand<5>(s, px, py, pz), cand<6>(s, px, py, pz),
+                     cand<7>(s, px, py, pz)};
+    lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
+  }
+  if (__ballot(cnt > 8u)) {
+    {
+      uint32_t u[4] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
+                       cand<11>(s, px, py, pz)};
+      lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
+    }
+    {
+      uint32_t u[4] = {cand<12>(s, px, py, pz), cand<13>(s, px, py, pz), cand<14>(s, px, py, pz),
+                       cand<15>(s, px, py, pz)};
+      lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
+    }
+  }
+#else
   {
     uint32_t u[8] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
                      cand<3>(s, px, py, pz), cand<4>(s, px, py, pz), cand<5>(s, px, py, pz),
                      cand<6>(s, px, py, pz), cand<7>(s, px, py, pz)};
-    lane_in = update8<MODE>(s, u, pool, lane);
+    lane_in = update8<MODE, 8>(s, u, pool, lane);
   }
   if (__ballot(cnt > 8u)) {
     uint32_t u[8] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
                      cand<11>(s, px, py, pz), cand<12>(s, px, py, pz), cand<13>(s, px, py, pz),
                      cand<14>(s, px, py, pz), cand<15>(s, px, py, pz)};
-    lane_in = update8<MODE>(s, u, pool, lane) || lane_in;
+    lane_in = update8<MODE, 8>(s, u, pool, lane) || lane_in;
   }
+#endif
   if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) hist_shrink(s, pool, lane, k);
   return lane_in;
 }
@@ -1063,7 +1099,7 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
   const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
-  // Row work-queue capacity 32 entries per row: 26 KB of LDS per 4-wave block, 6 blocks
+  // Row work-queue capacity 32 entries per row: 22 KB of LDS per 4-wave block, 7 blocks
   // per CU. LSK_ROWS_RCAP=64 selects the larger-queue instance (tuning experiments).
   static const int rcap = [] {
     const char *e = getenv("LSK_ROWS_RCAP");
