@@ -585,10 +585,8 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
   }
 
   if (valid) {
-    if (A.out_perm)
-      A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.ans));
-    else
-      A.out_d2[qi] = bitsf(s.ans);
+    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.ans));
+    if (A.out_d2) A.out_d2[qi] = bitsf(s.ans);
     if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
   }
 

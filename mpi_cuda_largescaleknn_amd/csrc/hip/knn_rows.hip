@@ -1030,10 +1030,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   }
 
   if (valid) {
-    if (A.out_perm)
-      A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.ans));
-    else
-      A.out_d2[qi] = bitsf(s.ans);
+    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.ans));
+    if (A.out_d2) A.out_d2[qi] = bitsf(s.ans);
 #ifdef LSK_PROFILE  // debug: wave cycles (>> 16) in place of the pass count
     if (A.qstatus)
       A.qstatus[qi] = qs | ((uint32_t)min((__builtin_readcyclecounter() - twave0) >> 16, (uint64_t)0xffff) << 16);

@@ -91,7 +91,7 @@ typedef struct lsk_knn_args {
   int32_t k;
   float cut2;               // (-r R)^2 as float; +inf by default
   float r_hint2;            // global estimate of the k-th squared distance
-  float *out_d2;            // [nq] k-th squared distance per query (sorted order)
+  float *out_d2;            // [nq] k-th squared distance per query (sorted order), or NULL
   unsigned long long *stats;  // optional [16] 64-bit counters (NULL = off)
   uint32_t *qstatus;        // optional [nq] per-query status bits (NULL = off)
   int32_t seed;             // queries are tree[0]'s points: seed pass 1 with buckets
@@ -100,9 +100,9 @@ typedef struct lsk_knn_args {
   const float *init_d2;     // optional [nq] known upper bound of each query's k-th squared
                             // distance (a re-query after a halo exchange passes the local
                             // result): the first range ends just above it (NULL = estimate)
-  const uint32_t *out_perm; // optional fused result scatter (single-rank path): when set,
-  float *out_final;         // out_final[out_perm[q]] = sqrtf(d2) (inf stays inf) is written
-                            // instead of out_d2[q] (saves the separate scatter kernel)
+  const uint32_t *out_perm; // optional fused result scatter: when set, the kernel also
+  float *out_final;         // writes out_final[out_perm[q]] = sqrtf(d2) (inf stays inf),
+                            // which saves a separate scatter kernel
 } lsk_knn_args;
 
 int lsk_hip_knn(const lsk_knn_args *args, void *stream);       // 64-query group kernel

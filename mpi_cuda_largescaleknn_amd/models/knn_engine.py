@@ -115,33 +115,48 @@ def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:
 def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalIndex | None = None,
           groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
-          init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None) -> torch.Tensor:
+          init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None,
+          keep_d2: bool = False) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
-    `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order, or —
-    with `final_out` — writes the final distances in input order (index.perm) straight
-    from the kernel (fused scatter) and returns final_out."""
+    `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order.
+
+    With `final_out` the kernel also writes the final distances in input order
+    (final_out[index.perm[q]], fused scatter); then the sorted d2 is only produced (and
+    returned) when `keep_d2` or `out` is given, else final_out is returned."""
     n = index.n
-    if out is None:
+    want_d2 = final_out is None or keep_d2 or out is not None
+    if out is None and want_d2:
         out = torch.empty(n, dtype=torch.float32, device=index.device)
     if n == 0:
-        return final_out if final_out is not None else out
-    if final_out is not None and not K.is_gpu(index.pts):
-        d2 = query(index, cfg, hint2, extra, groups, ngroups, out, stats, qstatus, init_d2)
-        return K.scatter1(d2, index.perm, final_out, finalize=True)
-    if K.is_gpu(index.pts):
-        trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
-        raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
-        K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
-                  stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL, init_d2=init_d2,
-                  out_perm=index.perm if final_out is not None else None, out_final=final_out)
-        if stats is not None:
-            stats.add(raw)
-        return final_out if final_out is not None else out
-    pts = index.pts[:n]
-    if extra is not None and extra.n > 0:
-        pts = torch.cat([pts, extra.pts[:extra.n]])
-    out.copy_(K.kth_cpu(pts, index.pts[:n], cfg.k, cfg.cut2))
-    return out
+        return out if want_d2 else final_out
+    if not K.is_gpu(index.pts):
+        if out is None:
+            out = torch.empty(n, dtype=torch.float32, device=index.device)
+        pts = index.pts[:n]
+        if extra is not None and extra.n > 0:
+            pts = torch.cat([pts, extra.pts[:extra.n]])
+        if groups is None:
+            out.copy_(K.kth_cpu(pts, index.pts[:n], cfg.k, cfg.cut2))
+            rows = None
+        else:
+            g = groups[:ngroups].to(torch.int64)
+            rows = (g[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
+            rows = rows[rows < n]
+            out[rows] = K.kth_cpu(pts, index.pts[:n][rows], cfg.k, cfg.cut2)
+        if final_out is not None:
+            if rows is None:
+                K.scatter1(out, index.perm, final_out, finalize=True)
+            else:
+                final_out[index.perm[rows].to(torch.int64)] = K.finalize_distances(out[rows])
+        return out if want_d2 else final_out
+    trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
+    raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
+    K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
+              stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL, init_d2=init_d2,
+              out_perm=index.perm if final_out is not None else None, out_final=final_out)
+    if stats is not None:
+        stats.add(raw)
+    return out if want_d2 else final_out
 
 
 def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,

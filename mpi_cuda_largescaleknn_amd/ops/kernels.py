@@ -221,8 +221,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     queries are trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
     init_d2 (optional, [nq]): a known upper bound of every query's k-th squared distance
     (e.g. the local result before a halo re-query) that places the first range.
-    out_perm / out_final (optional, fused scatter): the kernel writes
-    out_final[out_perm[q]] = final distance instead of out_d2[q] (out_d2 is then unused).
+    out_perm / out_final (optional, fused scatter): the kernel also writes
+    out_final[out_perm[q]] = final distance; out_d2 may then be None.
     """
     if (out_perm is None) != (out_final is None):
         raise ValueError("knn_gpu: out_perm and out_final go together")

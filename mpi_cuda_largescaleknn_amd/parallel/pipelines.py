@@ -182,8 +182,10 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
 
 
 def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig, hint2: float,
-                info: RunInfo) -> torch.Tensor:
-    """Exchange boundary candidates and re-query the affected query groups (exact)."""
+                info: RunInfo, final_out: torch.Tensor | None = None) -> torch.Tensor:
+    """Exchange boundary candidates and re-query the affected query groups (exact).
+    `final_out` (input order of index.perm) already holds the local final distances; the
+    re-query updates it in place together with the sorted d2."""
     size, rank = comm.size, comm.rank
     n = index.n
     dev = index.device
@@ -256,10 +258,10 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
             # the local k-th distance bounds the true one from above: the re-query starts
             # with a tight first range
             E.query(index, cfg, hint2, extra=hidx, groups=glist, ngroups=nflag, out=d2,
-                    stats=info.stats if cfg.collect_stats else None, init_d2=d2)
+                    stats=info.stats if cfg.collect_stats else None, init_d2=d2, final_out=final_out)
     else:
         info.timer.mark("halo_tree")
-        E.query(index, cfg, hint2, extra=hidx, out=d2)
+        E.query(index, cfg, hint2, extra=hidx, out=d2, final_out=final_out)
     info.timer.mark("halo_requery")
     return d2
 
@@ -291,11 +293,13 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
     index = E.build_index(owned, box)
     info.timer.mark("build")
-    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
-    info.timer.mark("knn_local")
-    d2 = halo_refine(index, d2, comm, cfg, hint2, info)
+    # final distances in received-row order straight from the kernels (fused scatter);
+    # the sorted d2 feeds the halo radii and the re-query bounds
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=points.device)
-    K.scatter1(d2, index.perm, dist_owned, finalize=True)
+    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None,
+                 final_out=dist_owned, keep_d2=True)
+    info.timer.mark("knn_local")
+    halo_refine(index, d2, comm, cfg, hint2, info, final_out=dist_owned)
     back, _ = comm.alltoallv(dist_owned, recv_counts)
     out = torch.empty(n_local, dtype=torch.float32, device=points.device)
     K.scatter1(back, send_perm, out, finalize=False)
@@ -325,9 +329,9 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
         E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
         info.timer.mark("knn_local")
         return out
-    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None)
+    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None,
+                 final_out=out, keep_d2=True)
     info.timer.mark("knn_local")
-    d2 = halo_refine(index, d2, comm, cfg, hint2, info)
-    K.scatter1(d2, index.perm, out, finalize=True)
+    halo_refine(index, d2, comm, cfg, hint2, info, final_out=out)
     info.timer.mark("return")
     return out

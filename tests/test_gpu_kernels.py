@@ -210,3 +210,28 @@ def test_fused_scatter_equals_separate_scatter(impl, monkeypatch):
     sep = K.scatter1(d2, idx.perm, torch.empty(idx.n, device=DEV), finalize=True)
     fused = E.query(idx, cfg, hint2, final_out=torch.full((idx.n,), -1.0, device=DEV))
     assert torch.equal(fused.cpu(), sep.cpu())
+
+
+def test_fused_scatter_keep_d2_and_group_requery():
+    """Multi-rank form: the kernel writes sorted d2 AND final distances in input order;
+    a group re-query updates both for its groups only."""
+    p = GENERATORS["uniform"](50000, seed=8).to(DEV)
+    idx = E.build_index(p)
+    cfg = E.KnnConfig(k=32)
+    hint2 = E.radius_hint2(idx.box, idx.n, 32)
+    ref_d2 = E.query(idx, cfg, hint2)
+    ref_fin = K.scatter1(ref_d2, idx.perm, torch.empty(idx.n, device=DEV), finalize=True)
+    fin = torch.full((idx.n,), -1.0, device=DEV)
+    d2 = E.query(idx, cfg, hint2, final_out=fin, keep_d2=True)
+    assert torch.equal(d2.cpu(), ref_d2.cpu()) and torch.equal(fin.cpu(), ref_fin.cpu())
+    groups = torch.arange(0, (idx.n + 63) // 64, 5, dtype=torch.int32, device=DEV)
+    d2b = torch.full((idx.n,), -1.0, device=DEV)
+    finb = torch.full((idx.n,), -1.0, device=DEV)
+    E.query(idx, cfg, hint2, groups=groups, ngroups=groups.numel(), out=d2b, final_out=finb)
+    sel = torch.zeros(idx.n, dtype=torch.bool, device=DEV)
+    for g in groups.tolist():
+        sel[g * 64:(g + 1) * 64] = True
+    assert torch.equal(d2b[sel].cpu(), ref_d2[sel].cpu()) and bool((d2b[~sel] == -1.0).all())
+    fsel = torch.zeros(idx.n, dtype=torch.bool, device=DEV)
+    fsel[idx.perm[sel].long()] = True
+    assert torch.equal(finb[fsel].cpu(), ref_fin[fsel].cpu()) and bool((finb[~fsel] == -1.0).all())
