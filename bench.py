@@ -49,6 +49,10 @@ def parse():
                     help="halo = MI355X pipeline; ring/peer = reference algorithm (ref-algo baseline)")
     ap.add_argument("--phases", action="store_true", help="print per-phase times (adds syncs)")
     ap.add_argument("--stats", action="store_true", help="collect k-NN kernel counters")
+    ap.add_argument("--direct-out", type=int, default=1,
+                    help="1 (default) = on one rank the k-NN kernel writes the distances straight "
+                         "into the pinned host buffer over PCIe while it runs (no device-to-host "
+                         "copy after it); 0 = device buffer + copy")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = rehearsal of the launch/timing contract (gloo, CPU oracle); "
                          "never a measurement")
@@ -119,10 +123,14 @@ def main():
         elif args.mode == "peer":
             out = RA.peer_knn(pts, comm, cfg, info)
         elif args.variant == "unordered":
-            out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total)
+            direct = bool(args.direct_out) and world == 1 and device.type == "cuda"
+            out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
+                                   out=host_out if direct else None)
         else:
-            out = PL.prepartitioned_knn(pts, comm, cfg, info)
-        host_out.copy_(out, non_blocking=True)
+            direct = bool(args.direct_out) and world == 1 and device.type == "cuda"
+            out = PL.prepartitioned_knn(pts, comm, cfg, info, out=host_out if direct else None)
+        if out.data_ptr() != host_out.data_ptr():
+            host_out.copy_(out, non_blocking=True)
         _sync(device)
         info_last = info
 

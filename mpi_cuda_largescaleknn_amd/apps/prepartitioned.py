@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import sys
 
+import torch
+
 from ..parallel import launch as L
 from ..parallel import pipelines as PL
 from ..parallel import refalgo as RA
@@ -51,8 +53,13 @@ def _run(args, launch, names) -> int:
         out = RA.peer_knn(dpts, launch.comm, cfg, info,
                           log=(lambda m: print(m, flush=True)))
     else:
-        out = PL.prepartitioned_knn(dpts, launch.comm, cfg, info)
+        # one GPU rank: the k-NN kernel writes the distances straight into pinned host memory
+        host_out = (torch.empty(pts.shape[0], dtype=torch.float32, pin_memory=True)
+                    if launch.device.type == "cuda" and launch.size == 1 else None)
+        out = PL.prepartitioned_knn(dpts, launch.comm, cfg, info, out=host_out)
     res = out.cpu()
+    if launch.device.type == "cuda":
+        torch.cuda.synchronize(launch.device)
     t1 = common.now(launch)
     print("done all queries...", flush=True)
     io.write_floats(output_name(args.output, launch.rank), res, 0, truncate=True)

@@ -44,8 +44,13 @@ def _run(args, launch) -> int:
     if args.mode == "ring":
         out = RA.ring_knn(dpts, launch.comm, cfg, info)
     else:
-        out = PL.unordered_knn(dpts, launch.comm, cfg, info, n_total=total)
+        # one GPU rank: the k-NN kernel writes the distances straight into pinned host memory
+        host_out = (torch.empty(pts.shape[0], dtype=torch.float32, pin_memory=True)
+                    if launch.device.type == "cuda" and launch.size == 1 else None)
+        out = PL.unordered_knn(dpts, launch.comm, cfg, info, n_total=total, out=host_out)
     res = out.cpu()
+    if launch.device.type == "cuda":
+        torch.cuda.synchronize(launch.device)
     t1 = common.now(launch)
     print("done all queries...", flush=True)
     # rank 0 creates/truncates and sizes the file, then every rank writes its block

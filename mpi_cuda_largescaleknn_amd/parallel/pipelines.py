@@ -267,10 +267,29 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
 
 
 # --------------------------------------------------------------------------- entrypoints
+def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.Tensor:
+    """Output buffer of a single-rank run: given (device tensor, or pinned host memory the
+    kernel writes over PCIe) or a new device tensor."""
+    if out is None:
+        return torch.empty(n, dtype=torch.float32, device=points.device)
+    if out.shape != (n,) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous float32 tensor with one entry per point")
+    if points.device.type == "cuda" and out.device.type == "cpu" and not out.is_pinned():
+        raise ValueError("a host output buffer for a GPU run must be pinned")
+    if points.device.type == "cpu" and out.device.type != "cpu":
+        raise ValueError("a CPU run needs a CPU output buffer")
+    return out
+
+
+
 def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
-                  n_total: int | None = None) -> torch.Tensor:
+                  n_total: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """k-th-NN distance of every local point (input order) for a globally unordered set
-    block-partitioned over ranks (reference unorderedData variant)."""
+    block-partitioned over ranks (reference unorderedData variant).
+
+    `out` (optional, float32 [n_local]): where the distances go. On one rank the k-NN
+    kernel writes them there directly — a pinned host tensor receives them straight over
+    PCIe while the kernel runs (no device-to-host copy afterwards)."""
     info = info or RunInfo(PhaseTimer(False, points.device))
     info.timer.start()
     points = points.contiguous()
@@ -286,7 +305,7 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
         index = E.build_index(points, box)
         info.timer.mark("build")
         # one rank: the k-NN kernel writes the final distances in input order (fused scatter)
-        out = torch.empty(n_local, dtype=torch.float32, device=points.device)
+        out = _check_out(out, n_local, points)
         E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
         info.timer.mark("knn_local")
         return out
@@ -301,16 +320,20 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     info.timer.mark("knn_local")
     halo_refine(index, d2, comm, cfg, hint2, info, final_out=dist_owned)
     back, _ = comm.alltoallv(dist_owned, recv_counts)
-    out = torch.empty(n_local, dtype=torch.float32, device=points.device)
-    K.scatter1(back, send_perm, out, finalize=False)
+    res = torch.empty(n_local, dtype=torch.float32, device=points.device)
+    K.scatter1(back, send_perm, res, finalize=False)
     info.timer.mark("return")
-    return out
+    if out is not None:
+        out.copy_(res, non_blocking=True)
+        return out
+    return res
 
 
 def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
-                       info: RunInfo | None = None) -> torch.Tensor:
+                       info: RunInfo | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """k-th-NN distance of every local point (input order) when each rank holds one
-    (spatially coherent) input file (reference prePartitionedData variant)."""
+    (spatially coherent) input file (reference prePartitionedData variant). `out` as in
+    unordered_knn (on one rank a pinned host tensor is written by the kernel directly)."""
     info = info or RunInfo(PhaseTimer(False, points.device))
     info.timer.start()
     points = points.contiguous()
@@ -324,14 +347,18 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     info.timer.mark("bounds")
     index = E.build_index(points, box)
     info.timer.mark("build")
-    out = torch.empty(n_local, dtype=torch.float32, device=points.device)
     if comm.size == 1:  # fused scatter: final distances straight from the k-NN kernel
+        out = _check_out(out, n_local, points)
         E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
         info.timer.mark("knn_local")
         return out
+    res = torch.empty(n_local, dtype=torch.float32, device=points.device)
     d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None,
-                 final_out=out, keep_d2=True)
+                 final_out=res, keep_d2=True)
     info.timer.mark("knn_local")
-    halo_refine(index, d2, comm, cfg, hint2, info, final_out=out)
+    halo_refine(index, d2, comm, cfg, hint2, info, final_out=res)
     info.timer.mark("return")
-    return out
+    if out is not None:
+        out.copy_(res, non_blocking=True)
+        return out
+    return res

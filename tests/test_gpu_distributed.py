@@ -88,3 +88,21 @@ def test_cutoff_multirank_gpu():
             return PL.unordered_knn(p[b:e].to(DEV), comm, E.KnnConfig(k=k, max_radius=r)).cpu()
 
         assert torch.equal(torch.cat(run_loopback(3, fn, DEV)), ref)
+
+
+def test_single_rank_direct_host_output():
+    """One rank: the k-NN kernel writes into a pinned host buffer over PCIe (bench
+    default); same bits as the device buffer + copy, for both entrypoints."""
+    from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm
+    p = clustered(120_000, seed=4)
+    cfg = E.KnnConfig(k=40)
+    comm = SingleComm(DEV)
+    for fn in (PL.unordered_knn, PL.prepartitioned_knn):
+        ref = fn(p.to(DEV), comm, cfg).cpu()
+        host = torch.full((p.shape[0],), -1.0).pin_memory()
+        got = fn(p.to(DEV), comm, cfg, out=host)
+        torch.cuda.synchronize()
+        assert got.data_ptr() == host.data_ptr()
+        assert torch.equal(host, ref)
+    with pytest.raises(ValueError):
+        PL.unordered_knn(p.to(DEV), comm, cfg, out=torch.empty(p.shape[0]))  # not pinned
