@@ -340,16 +340,19 @@ __device__ __forceinline__ lsk_tree_view pick_tree(const lsk_knn_args &A, uint32
 // Branch-free (the load is always issued, from a clamped in-bounds address), so the
 // compiler can count outstanding loads and the prefetch is not serialised by vmcnt(0).
 // 32-bit index math (trees hold < 2^31 points, checked on the host).
+// NT = number of trees the kernel instance handles (1: no per-lane tree selects).
+template <int NT>
 __device__ __forceinline__ uint32_t load_quarter(const WaveCtx &W, uint32_t e, float &px, float &py,
                                                  float &pz) {
   const bool ok = e != kInvalid;
-  const bool t1 = (e >> 31) != 0;
+  const bool t1 = NT > 1 && (e >> 31) != 0;
   const uint32_t n = t1 ? W.n1 : W.n0;
   const uint32_t q16 = (e & 0x7fffffffu) << 4;
   const uint32_t idx = q16 | (uint32_t)(W.lane & 15);
   const bool live = ok && idx < n;
   // dead lanes read point 0 of a non-empty tree
-  const float *p = live ? (t1 ? W.p1 : W.p0) + 3u * idx : W.pdef;
+  const float *p = NT == 1 ? W.p0 + 3u * (live ? idx : 0u)
+                           : (live ? (t1 ? W.p1 : W.p0) + 3u * idx : W.pdef);
   px = p[0];  // raw: the consumer substitutes +inf for padding lanes (see process_steps)
   py = p[1];
   pz = p[2];
@@ -368,7 +371,7 @@ __device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
 }
 
 // n lockstep steps: every row consumes its head entry (rows with an empty queue idle).
-template <int MODE>
+template <int MODE, int NT>
 __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn_args &A,
                                               uint32_t n) {
   n = lsk::uniform(n);  // wave-uniform loop (lets the compiler keep it scalar)
@@ -376,7 +379,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
   // one step of prefetch; loads are unconditional (the entry after the last step is
   // fetched too, harmlessly) so no branch breaks the compiler's count of outstanding loads
   float px, py, pz;
-  uint32_t cnt = load_quarter(W, row_entry(W, W.rhead), px, py, pz);
+  uint32_t cnt = load_quarter<NT>(W, row_entry(W, W.rhead), px, py, pz);
   // (two steps of prefetch: 0.155 vs 0.152 s at 6 waves/SIMD with 10 spilled VGPRs,
   // 0.166 s at 5 waves/SIMD — occupancy, not the candidate-load distance, is what counts)
   const float inf = __builtin_inff();
@@ -385,7 +388,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     const bool live = (uint32_t)(W.lane & 15) < ccnt;
     const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
     W.rhead += W.rhead < W.rlen ? 1u : 0u;
-    cnt = load_quarter(W, row_entry(W, W.rhead), px, py, pz);
+    cnt = load_quarter<NT>(W, row_entry(W, W.rhead), px, py, pz);
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
 #ifdef LSK_PROFILE
@@ -561,7 +564,7 @@ __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preservi
 //  * replay (pass > 1 with a complete pass-1 log): the pre-leaf nodes and per-quarter
 //    row masks come from the log instead of the walk (bounds only shrink after pass 1,
 //    so the log is a superset of what later passes need).
-template <int MODE, bool replay>
+template <int MODE, bool replay, int NT>
 __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args &A) {
   const lsk::vec3f q{s.qx, s.qy, s.qz};
   const lsk::vec3f c{W.cx, W.cy, W.cz};
@@ -760,7 +763,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     const uint32_t mxp = max_pend(W), mnp = min_pend(W);
     const uint32_t nsteps = finished ? mxp : overflow ? max(mnp, mxp + 8u - min(mxp + 8u, W.rcap)) : mnp;
     LSK_PT(tp0);
-    process_steps<MODE>(s, W, A, nsteps);
+    process_steps<MODE, NT>(s, W, A, nsteps);
     LSK_PADD(W.prof[MODE], tp0);
   }
 }
@@ -815,7 +818,7 @@ enum : uint32_t {
   QS_HINT = 1024
 };
 
-template <int RCAP>
+template <int RCAP, int NT>
 __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_rows_kernel(const lsk_knn_args A) {
   __shared__ WaveLdsR<RCAP> lds[kWavesPerBlock];
   const int wid = threadIdx.x >> 6;
@@ -960,9 +963,9 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       if (first) W.log_ok = true;
       LSK_PT(tt0);
       if (!first && W.log_ok)
-        traverse<MODE_HIST, true>(s, W, A);
+        traverse<MODE_HIST, true, NT>(s, W, A);
       else
-        traverse<MODE_HIST, false>(s, W, A);
+        traverse<MODE_HIST, false, NT>(s, W, A);
       LSK_PADD(W.prof[2], tt0);
       W.logging = false;
       first = false;
@@ -1040,9 +1043,9 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     s.ccnt = 0;
     LSK_PT(tc0);
     if (W.log_ok)
-      traverse<MODE_COLLECT, true>(s, W, A);
+      traverse<MODE_COLLECT, true, NT>(s, W, A);
     else
-      traverse<MODE_COLLECT, false>(s, W, A);
+      traverse<MODE_COLLECT, false, NT>(s, W, A);
     LSK_PADD(W.prof[3], tc0);
     LSK_PT(ts0);
     if (s.state == ST_READY) {
@@ -1137,15 +1140,12 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   if (ngroups <= 0) return 0;
   const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
   // Row work-queue capacity 32 entries per row: 22 KB of LDS per 4-wave block, 7 blocks
-  // per CU. LSK_ROWS_RCAP=64 selects the larger-queue instance (tuning experiments).
-  static const int rcap = [] {
-    const char *e = getenv("LSK_ROWS_RCAP");
-    return e ? atoi(e) : 32;
-  }();
-  if (rcap == 64)
-    knn_rows_kernel<64><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+  // per CU. One instance per tree count: the single-tree one (every local pass) has no
+  // per-lane tree selects in its step loop; the two-tree one serves halo re-queries.
+  if (A.ntrees > 1)
+    knn_rows_kernel<32, 2><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   else
-    knn_rows_kernel<32><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+    knn_rows_kernel<32, 1><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   LSK_CHECK_LAUNCH("knn_rows");
   return 0;
 }
