@@ -90,12 +90,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.device == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # one rank per GPU (ranks beyond the device count wrap: rehearsals with
+        # LSKNN_DIST_BACKEND=gloo only, RCCL refuses two ranks on one GPU)
+        dev_id = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_id)
+        device = torch.device("cuda", dev_id)
     else:
         device = torch.device("cpu")
     if world > 1:
-        if device.type == "cuda":
+        if device.type == "cuda" and os.environ.get("LSKNN_DIST_BACKEND", "nccl") == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")

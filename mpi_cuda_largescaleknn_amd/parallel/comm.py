@@ -98,7 +98,11 @@ _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp
 
 
 class TorchComm(Comm):
-    """torch.distributed process group (RCCL for GPU tensors, gloo for CPU)."""
+    """torch.distributed process group (RCCL for GPU tensors, gloo for CPU).
+
+    A gloo group with GPU-resident data (several processes sharing one GPU: RCCL refuses
+    two ranks on one device) stages every collective through host memory, so the whole
+    multi-process GPU pipeline can run on a one-GPU box (tests/test_gpu_multiprocess.py)."""
 
     def __init__(self, device: torch.device | str, group=None):
         self.group = group
@@ -106,6 +110,7 @@ class TorchComm(Comm):
         self.size = dist.get_world_size(group)
         self._device = torch.device(device)
         self.backend = dist.get_backend(group)
+        self.staged = self.backend == "gloo" and self._device.type != "cpu"
 
     @property
     def device(self) -> torch.device:
@@ -113,35 +118,53 @@ class TorchComm(Comm):
 
     def allreduce_(self, t, op="sum"):
         if self.size > 1:
-            dist.all_reduce(t, op=_OPS[op], group=self.group)
+            if self.staged and t.device.type != "cpu":
+                h = t.cpu()
+                dist.all_reduce(h, op=_OPS[op], group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=_OPS[op], group=self.group)
         return t
 
     def allgather(self, t):
         t = t.contiguous()
-        out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
+        if self.staged and t.device.type != "cpu" and self.size > 1:
+            return self._gather_gloo(t.cpu()).to(t.device)
         if self.size == 1:
+            out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
             out[0].copy_(t)
-        elif self.backend == "gloo":
-            dist.all_gather(list(out.unbind(0)), t, group=self.group)
-        else:
-            dist.all_gather_into_tensor(out, t, group=self.group)
+            return out
+        if self.backend == "gloo":
+            return self._gather_gloo(t)
+        out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
+    def _gather_gloo(self, t):
+        out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather(list(out.unbind(0)), t, group=self.group)
         return out
 
     def alltoallv(self, send, send_counts):
         send_counts = [int(c) for c in send_counts]
         recv_counts = self.exchange_counts(send_counts)
         row_shape = tuple(send.shape[1:])
-        recv = torch.empty((sum(recv_counts), *row_shape), dtype=send.dtype, device=send.device)
         if self.size == 1:
-            recv.copy_(send)
-        else:
-            dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=recv_counts,
-                                   input_split_sizes=send_counts, group=self.group)
-        return recv, recv_counts
+            return send.clone(), recv_counts
+        dev = send.device
+        staged = self.staged and dev.type != "cpu"
+        src = send.cpu() if staged else send.contiguous()
+        recv = torch.empty((sum(recv_counts), *row_shape), dtype=send.dtype, device=src.device)
+        dist.all_to_all_single(recv, src, output_split_sizes=recv_counts,
+                               input_split_sizes=send_counts, group=self.group)
+        return (recv.to(dev) if staged else recv), recv_counts
 
     def p2p(self, sends, recvs):
-        out = [torch.empty(shape, dtype=dt, device=self._device) for _, shape, dt in recvs]
-        ops = [dist.P2POp(dist.isend, t.contiguous(), dst, group=self.group) for dst, t in sends if dst != self.rank]
+        staged = self.staged
+        bufdev = torch.device("cpu") if staged else self._device
+        out = [torch.empty(shape, dtype=dt, device=bufdev) for _, shape, dt in recvs]
+        ops = [dist.P2POp(dist.isend, (t.cpu() if staged else t.contiguous()), dst, group=self.group)
+               for dst, t in sends if dst != self.rank]
         ops += [dist.P2POp(dist.irecv, buf, src, group=self.group)
                 for (src, _, _), buf in zip(recvs, out) if src != self.rank]
         own = {dst: t for dst, t in sends if dst == self.rank}
@@ -151,7 +174,7 @@ class TorchComm(Comm):
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        return out
+        return [b.to(self._device) for b in out] if staged else out
 
     def barrier(self):
         if self.size > 1:
@@ -161,6 +184,8 @@ class TorchComm(Comm):
                 dist.all_reduce(t, group=self.group)
                 torch.cuda.synchronize(self._device)
             else:
+                if self._device.type == "cuda":
+                    torch.cuda.synchronize(self._device)
                 dist.barrier(group=self.group)
 
 

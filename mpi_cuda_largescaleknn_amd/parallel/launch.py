@@ -13,6 +13,11 @@ Accepted launchers (all run the same code):
 Device selection follows the reference's ``-g G`` (device = rank % G,
 unorderedDataVariant.cu:138-143); without ``-g`` the local rank picks the device
 (the reference would put every rank on GPU 0).
+
+The process group is RCCL (``nccl``) for GPU runs and gloo for CPU runs.
+``LSKNN_DIST_BACKEND=gloo`` forces gloo with GPU data (collectives staged through host
+memory, see TorchComm): the only way to run several GPU ranks on one device, since RCCL
+refuses two ranks on the same GPU.
 """
 from __future__ import annotations
 
@@ -71,7 +76,12 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         # collective timeout = watchdog timeout; RCCL errors surface asynchronously
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = datetime.timedelta(seconds=F.timeout_s())
-        if use_gpu:
+        backend = os.environ.get("LSKNN_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+        if backend not in ("nccl", "gloo"):
+            raise ValueError(f"LSKNN_DIST_BACKEND must be nccl or gloo, not {backend!r}")
+        if backend == "nccl":
+            if not use_gpu:
+                raise ValueError("LSKNN_DIST_BACKEND=nccl needs a GPU run")
             dist.init_process_group("nccl", rank=rank, world_size=size, device_id=device, timeout=timeout)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
