@@ -49,10 +49,11 @@ def parse():
                     help="halo = MI355X pipeline; ring/peer = reference algorithm (ref-algo baseline)")
     ap.add_argument("--phases", action="store_true", help="print per-phase times (adds syncs)")
     ap.add_argument("--stats", action="store_true", help="collect k-NN kernel counters")
-    ap.add_argument("--direct-out", type=int, default=1,
-                    help="1 (default) = on one rank the k-NN kernel writes the distances straight "
-                         "into the pinned host buffer over PCIe while it runs (no device-to-host "
-                         "copy after it); 0 = device buffer + copy")
+    ap.add_argument("--direct-out", type=int, default=-1,
+                    help="1 = on one rank the k-NN kernel writes the distances straight into the "
+                         "pinned host buffer over PCIe while it runs (no device-to-host copy after "
+                         "it); 0 = device buffer + copy; -1 (default) = 1 when k >= 48 (where the "
+                         "PCIe writes hide under the kernel, pipelines.direct_host_out_pays)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = rehearsal of the launch/timing contract (gloo, CPU oracle); "
                          "never a measurement")
@@ -112,6 +113,8 @@ def main():
     host_out = torch.empty(host_pts.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda")
 
     info_last = None
+    direct = (PL.direct_host_out_pays(args.k) if args.direct_out < 0 else bool(args.direct_out)) \
+        and world == 1 and device.type == "cuda"
 
     def step():
         with trace.range("lsknn:step"):
@@ -126,11 +129,9 @@ def main():
         elif args.mode == "peer":
             out = RA.peer_knn(pts, comm, cfg, info)
         elif args.variant == "unordered":
-            direct = bool(args.direct_out) and world == 1 and device.type == "cuda"
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
                                    out=host_out if direct else None)
         else:
-            direct = bool(args.direct_out) and world == 1 and device.type == "cuda"
             out = PL.prepartitioned_knn(pts, comm, cfg, info, out=host_out if direct else None)
         if out.data_ptr() != host_out.data_ptr():
             host_out.copy_(out, non_blocking=True)

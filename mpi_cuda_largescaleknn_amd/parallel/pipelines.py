@@ -267,6 +267,19 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
 
 
 # --------------------------------------------------------------------------- entrypoints
+# Single-rank runs can let the k-NN kernel write the distances straight into pinned host
+# memory (random 4-byte PCIe writes at perm[q], hidden under the kernel) instead of a
+# device buffer + copy. The writes sustain ~0.9-1e9 points/s: they hide under the kernel
+# only when it is slow enough per point, i.e. from k ~ 48 (1e8 uniform points on one
+# MI355X, step ms copy/direct: k=16 118/172, k=48 141/135, k=64 151/145, k=100
+# 176/170; 1e7 k=16 12.5/17.9; profiles/r1_v20/direct_out_ab.txt).
+DIRECT_OUT_MIN_K = 48
+
+
+def direct_host_out_pays(k: int) -> bool:
+    return k >= DIRECT_OUT_MIN_K
+
+
 def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.Tensor:
     """Output buffer of a single-rank run: given (device tensor, or pinned host memory the
     kernel writes over PCIe) or a new device tensor."""
