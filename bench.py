@@ -31,7 +31,7 @@ from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm  # noqa: E402
-from mpi_cuda_largescaleknn_amd.utils import trace  # noqa: E402
+from mpi_cuda_largescaleknn_amd.utils import numa, trace  # noqa: E402
 
 METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -96,6 +96,10 @@ def main():
         dev_id = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_id)
         device = torch.device("cuda", dev_id)
+        # host side (pinned input/output buffers) on the GPU's NUMA node
+        bound = numa.bind_to_device(device)
+        if bound and args.phases:
+            print(f"rank {rank}: bound to {bound}", file=sys.stderr)
     else:
         device = torch.device("cpu")
     if world > 1:

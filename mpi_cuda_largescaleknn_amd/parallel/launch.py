@@ -28,6 +28,7 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from ..utils import numa
 from . import faults as F
 from .comm import Comm, SingleComm, TorchComm
 
@@ -65,6 +66,10 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
             print(f"#{rank}/{size}setting active GPU #{dev_id}", flush=True)
         torch.cuda.set_device(dev_id)
         device = torch.device("cuda", dev_id)
+        # before any pinned allocation: host buffers land on the GPU's NUMA node
+        bound = numa.bind_to_device(device)
+        if bound and verbose:
+            print(f"#{rank}/{size}: bound to {bound}", flush=True)
     else:
         device = torch.device("cpu")
     fault = F.parse_fault(os.environ.get("LSKNN_FAULT"))
