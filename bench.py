@@ -54,6 +54,10 @@ def parse():
                          "pinned host buffer over PCIe while it runs (no device-to-host copy after "
                          "it); 0 = device buffer + copy; -1 (default) = 1 when k >= 48 (where the "
                          "PCIe writes hide under the kernel, pipelines.direct_host_out_pays)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1 = capture the whole single-rank step (H2D, index build, k-NN, results "
+                         "to host) in one HIP graph after the warmup and replay it per step; "
+                         "0 = eager launches; -1 (default) = 1 on one GPU rank without --phases/--stats")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = rehearsal of the launch/timing contract (gloo, CPU oracle); "
                          "never a measurement")
@@ -123,6 +127,7 @@ def main():
     def step():
         with trace.range("lsknn:step"):
             _step()
+            _sync(device)
 
     def _step():
         nonlocal info_last
@@ -139,11 +144,35 @@ def main():
             out = PL.prepartitioned_knn(pts, comm, cfg, info, out=host_out if direct else None)
         if out.data_ptr() != host_out.data_ptr():
             host_out.copy_(out, non_blocking=True)
-        _sync(device)
         info_last = info
 
-    for _ in range(args.warmup):
-        step()
+    use_graph = (args.graph == 1 or (args.graph < 0 and not (args.phases or args.stats))) \
+        and world == 1 and device.type == "cuda" and args.mode == "halo"
+    graph = None
+    if use_graph:
+        # warm up on a side stream (allocator + library state), then capture one whole
+        # step — every launch and both host copies — into a graph replayed per step: the
+        # single-rank pipeline has no host round trip (device-side radius hint), so the
+        # replay does the same work as an eager step minus the per-launch CPU overhead
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, args.warmup)):
+                _step()
+        torch.cuda.current_stream(device).wait_stream(side)
+        _sync(device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            _step()
+        _sync(device)
+
+        def step():  # noqa: F811 — graph replay replaces the eager step
+            with trace.range("lsknn:step"):
+                graph.replay()
+                _sync(device)
+    else:
+        for _ in range(args.warmup):
+            step()
     comm.barrier()
     _sync(device)
     t0 = time.perf_counter()
@@ -185,6 +214,7 @@ def main():
                                 f"spatial-redistribute+halo x{world}" if args.variant == "unordered"
                                 else f"halo x{world}"),
                 "k": args.k,
+                "hip_graph": graph is not None,
                 "all_finite": finite,
             },
         }

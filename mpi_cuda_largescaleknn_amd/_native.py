@@ -55,7 +55,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 2  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 3  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -125,6 +125,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_bounds_ws_bytes": ([i64], C.c_size_t),
         "lsk_hip_bounds": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_box_finalize": ([vp, vp], i32),
+        "lsk_hip_radius_hint": ([vp, i64, i32, vp, vp], i32),
         "lsk_hip_morton": ([vp, i64, vp, vp, vp, i32, vp], i32),
         "lsk_hip_gather3": ([vp, vp, i64, vp, vp], i32),
         "lsk_hip_scatter1": ([vp, vp, i64, vp, i32, vp], i32),

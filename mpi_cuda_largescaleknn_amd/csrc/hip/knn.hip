@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kThreads) void knn_kernel(const lsk_knn_args A) {
     if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
   }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
-    r_est2 = A.r_hint2;
+    r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
     qs |= QS_HINT;
   }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) r_est2 = 1.f;

@@ -23,6 +23,9 @@ extern "C" {
 #endif
 
 int lsk_hip_abi_version(void);
+// Uniform-density estimate of the k-th squared distance from a bounds box [8] and the
+// global point count, written to out[0] on the device (= knn_engine.radius_hint2).
+int lsk_hip_radius_hint(const float *box, int64_t n_total, int32_t k, float *out, void *stream);
 const char *lsk_hip_last_error(void);
 int lsk_hip_device_info(int device, char *buf, int buflen);
 
@@ -90,7 +93,9 @@ typedef struct lsk_knn_args {
   int32_t ntrees;
   int32_t k;
   float cut2;               // (-r R)^2 as float; +inf by default
-  float r_hint2;            // global estimate of the k-th squared distance
+  float r_hint2;            // global estimate of the k-th squared distance; < 0: read it
+                            // from tree[0].nodes[3] (the unused node 0, where
+                            // lsk_hip_radius_hint's value was copied: no host round trip)
   float *out_d2;            // [nq] k-th squared distance per query (sorted order), or NULL
   unsigned long long *stats;  // optional [16] 64-bit counters (NULL = off)
   uint32_t *qstatus;        // optional [nq] per-query status bits (NULL = off)

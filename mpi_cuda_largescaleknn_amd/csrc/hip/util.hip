@@ -17,7 +17,7 @@ void set_last_error(const std::string &msg) {
 }
 }  // namespace lsk
 
-extern "C" int lsk_hip_abi_version(void) { return 2; }
+extern "C" int lsk_hip_abi_version(void) { return 3; }
 
 extern "C" const char *lsk_hip_last_error(void) {
   static thread_local std::string copy;
@@ -93,6 +93,31 @@ __global__ void bounds_final_kernel(const float *__restrict__ partial, int nb,
 
 __global__ void box_finalize_kernel(float *box) {
   if (threadIdx.x == 0) finalize_box(box);
+}
+
+// k-th-distance estimate for uniform density over the box's non-degenerate axes
+// (knn_engine.radius_hint2; only used by groups of zero extent, so it need not match the
+// host value bit for bit). 1 when nothing is known.
+__global__ void radius_hint_kernel(const float *box, int64_t n_total, int32_t k, float *out) {
+  if (threadIdx.x != 0) return;
+  double measure = 1.0;
+  int dim = 0;
+  bool ok = n_total > 0;
+  for (int a = 0; a < 3; a++) {
+    const double e = (double)box[3 + a] - (double)box[a];
+    if (!(e == e) || e == __builtin_inf() || e == -__builtin_inf()) ok = false;
+    if (e > 0.0) {
+      measure *= e;
+      dim++;
+    }
+  }
+  float r2 = 1.f;
+  if (ok && dim > 0) {
+    const double unit = dim == 1 ? 2.0 : dim == 2 ? 3.14159265358979323846 : 4.0 * 3.14159265358979323846 / 3.0;
+    const double r = pow((double)k / (unit * ((double)n_total / measure)), 1.0 / dim);
+    r2 = (float)(r * r);
+  }
+  out[0] = r2;
 }
 
 __global__ __launch_bounds__(256) void morton_kernel(const float *__restrict__ pts, int64_t n,
@@ -199,6 +224,13 @@ extern "C" int lsk_hip_bounds(const float *pts, int64_t n, float *box_out, void 
   LSK_CHECK_LAUNCH("bounds_partial");
   bounds_final_kernel<<<1, 64, 0, s>>>((const float *)ws, (int)nb, box_out);
   LSK_CHECK_LAUNCH("bounds_final");
+  return 0;
+}
+
+extern "C" int lsk_hip_radius_hint(const float *box, int64_t n_total, int32_t k, float *out,
+                                   void *stream) {
+  radius_hint_kernel<<<1, 64, 0, (hipStream_t)stream>>>(box, n_total, k, out);
+  LSK_CHECK_LAUNCH("radius_hint");
   return 0;
 }
 

@@ -112,7 +112,16 @@ def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:
     return float(r * r)
 
 
-def query(index: LocalIndex, cfg: KnnConfig, hint2: float = 0.0, extra: LocalIndex | None = None,
+def radius_hint(box: torch.Tensor, n_total: int, k: int) -> float | torch.Tensor:
+    """radius_hint2 without a host round trip: for a GPU box a 1-element device tensor
+    computed by a kernel (the k-NN kernel reads it in place), else the host float. Keeps
+    the single-rank pipeline free of device->host syncs (HIP-graph capturable)."""
+    if K.is_gpu(box):
+        return K.radius_hint(box, n_total, k)
+    return radius_hint2(box, n_total, k)
+
+
+def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, extra: LocalIndex | None = None,
           groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
           init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None,
@@ -165,6 +174,6 @@ def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,
     (itself counted), in input order — the single-rank reference output."""
     cfg = KnnConfig(k=k, max_radius=max_radius)
     index = build_index(points)
-    hint2 = radius_hint2(index.box, index.n, k)
+    hint2 = radius_hint(index.box, index.n, k)
     out = torch.empty(index.n, dtype=torch.float32, device=points.device)
     return query(index, cfg, hint2, stats=stats, final_out=out)

@@ -209,7 +209,16 @@ def tree_set_radii(nodes: torch.Tensor, n: int, d2_sorted: torch.Tensor) -> torc
 
 
 # --------------------------------------------------------------------------- kNN
-def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hint2: float,
+def radius_hint(box: torch.Tensor, n_total: int, k: int) -> torch.Tensor:
+    """Device [1] float32: uniform-density k-th squared distance estimate of a GPU box."""
+    out = torch.empty(1, dtype=torch.float32, device=box.device)
+    check(_native.hip().lsk_hip_radius_hint(_ptr(box), int(n_total), int(k), _ptr(out), _stream(box)),
+          "radius_hint")
+    return out
+
+
+def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
+            r_hint2: float | torch.Tensor,
             out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
@@ -239,7 +248,13 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float, r_hin
     a.ntrees = len(trees)
     a.k = k
     a.cut2 = cut2
-    a.r_hint2 = r_hint2
+    if isinstance(r_hint2, torch.Tensor):
+        # device value (K.radius_hint): parked in the unused node 0 of tree 0, which the
+        # kernel reads when r_hint2 < 0 — no host round trip, no extra kernel argument
+        trees[0][1].view(-1)[3:4].copy_(r_hint2.view(-1)[:1])
+        a.r_hint2 = -1.0
+    else:
+        a.r_hint2 = max(float(r_hint2), 0.0)
     a.out_d2 = _ptr(out_d2)
     a.stats = _ptr(stats)
     a.qstatus = _ptr(qstatus)

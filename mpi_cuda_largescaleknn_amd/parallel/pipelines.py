@@ -181,7 +181,8 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
     return recv, recv_counts, perm, send_counts
 
 
-def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig, hint2: float,
+def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
+                hint2: float | torch.Tensor,
                 info: RunInfo, final_out: torch.Tensor | None = None) -> torch.Tensor:
     """Exchange boundary candidates and re-query the affected query groups (exact).
     `final_out` (input order of index.perm) already holds the local final distances; the
@@ -312,7 +313,7 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
         comm.allreduce_(t, "sum")
         n_total = int(t.item())
     box = global_box(points, comm)
-    hint2 = E.radius_hint2(box, n_total, cfg.k)
+    hint2 = E.radius_hint(box, n_total, cfg.k)
     info.timer.mark("bounds")
     if comm.size == 1:
         index = E.build_index(points, box)
@@ -351,12 +352,15 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     info.timer.start()
     points = points.contiguous()
     n_local = points.shape[0]
-    t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
-    comm.allreduce_(t, "sum")
-    n_total = int(t.item())
+    if comm.size == 1:
+        n_total = n_local
+    else:
+        t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
+        comm.allreduce_(t, "sum")
+        n_total = int(t.item())
     box = K.bounds(points)
-    gbox = global_box(points, comm)
-    hint2 = E.radius_hint2(gbox, n_total, cfg.k)
+    gbox = global_box(points, comm) if comm.size > 1 else box
+    hint2 = E.radius_hint(gbox, n_total, cfg.k)
     info.timer.mark("bounds")
     index = E.build_index(points, box)
     info.timer.mark("build")

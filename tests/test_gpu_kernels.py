@@ -24,7 +24,7 @@ def oracle(points, k, max_radius=math.inf, method="kdtree"):
 def test_native_library_is_loaded():
     from mpi_cuda_largescaleknn_amd import _native
     lib = _native.hip()
-    assert lib.lsk_hip_abi_version() == 2
+    assert lib.lsk_hip_abi_version() == 3
     import ctypes as C
     buf = C.create_string_buffer(512)
     assert lib.lsk_hip_device_info(0, buf, 512) == 0
