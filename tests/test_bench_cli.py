@@ -41,6 +41,20 @@ def test_bench_single_rank_cpu():
     assert rec["config"]["all_finite"] is True
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_bench_single_gpu_graph_and_eager(graph):
+    """The driver's default single-GPU bench path: the step captured as a HIP graph (or
+    eager), distances finite, the graph flag reported."""
+    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "3", "--warmup", "1",
+                          "--graph", graph], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
+    assert rec["config"]["all_finite"] is True
+    assert rec["config"]["hip_graph"] is (graph == "1")
+
+
 @pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])
 def test_bench_two_ranks_torchrun_gloo(variant):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
