@@ -11,15 +11,39 @@
 
 namespace {
 
+// 16-lane row reductions on DPP (VALU, a few cycles each) instead of LDS-routed
+// shuffles: quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_ror:4, row_ror:8 — afterwards
+// every lane of the row holds the row's min / max.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float min16(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
-  return v;
+  v = fminf(v, dppf<0xB1>(v));
+  v = fminf(v, dppf<0x4E>(v));
+  v = fminf(v, dppf<0x124>(v));
+  return fminf(v, dppf<0x128>(v));
 }
 __device__ __forceinline__ float max16(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x124>(v));
+  return fmaxf(v, dppf<0x128>(v));
+}
+// bucket value from the four row values (lanes 0, 16, 32, 48), on the scalar side
+__device__ __forceinline__ float rows_min(float v) {
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fminf(fminf(a, b), fminf(c, d));
+}
+__device__ __forceinline__ float rows_max(float v) {
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(a, b), fmaxf(c, d));
 }
 
 // One wave per 64-point bucket: the leaf box and (optionally) the four 16-point
@@ -47,8 +71,8 @@ __global__ __launch_bounds__(256) void leaf_kernel(const float *__restrict__ pts
     qd[0] = make_float4(lx, ly, lz, 0.f);
     qd[1] = make_float4(hx, hy, hz, 0.f);
   }
-  lx = lsk::wave_min(lx); ly = lsk::wave_min(ly); lz = lsk::wave_min(lz);
-  hx = lsk::wave_max(hx); hy = lsk::wave_max(hy); hz = lsk::wave_max(hz);
+  lx = rows_min(lx); ly = rows_min(ly); lz = rows_min(lz);
+  hx = rows_max(hx); hy = rows_max(hy); hz = rows_max(hz);
   if (lane == 0) {
     float4 *nd = (float4 *)nodes + 2 * (((int64_t)1 << depth) + leaf);
     nd[0] = make_float4(lx, ly, lz, 0.f);
@@ -81,7 +105,7 @@ __global__ __launch_bounds__(256) void leaf_radius_kernel(const float *__restric
   if (leaf >= nleaf_slots) return;
   const int64_t i = leaf * lsk::kBucket + lsk::lane_id();
   float r = i < n ? d2[i] : 0.f;
-  r = lsk::wave_max(r);
+  r = rows_max(max16(r));
   if (lsk::lane_id() == 0) nodes[8 * (((int64_t)1 << depth) + leaf) + 3] = r;
 }
 
