@@ -90,7 +90,12 @@ HIST_SAMPLE = 8   # splitter histogram over every 8th key of ranks holding >= 2^
 def _hist_sample(n: int) -> int:
     """Key sampling stride of the splitter histogram (balance only; exactness does not
     depend on the splitters)."""
-    return HIST_SAMPLE if n >= (1 << 20) else 1
+    if n < (1 << 20):
+        return 1
+    # at most ~8M sampled keys: their atomics into the shared histogram cost 2.6 ms per
+    # 500M-point rank at stride 8 (profiles/r1_v20/lb_scaling), and 8M samples already
+    # place the splitters far inside the 2 % tolerance
+    return max(HIST_SAMPLE, n >> 23)
 
 
 def _splitters(hist: torch.Tensor, total: int, size: int) -> list[int]:
