@@ -230,3 +230,22 @@ def test_hilbert_cell_block_is_a_face_connected_path(corner):
 def test_morton_key_bit_interleave():
     c = torch.tensor([[1, 0, 0], [0, 1, 0], [0, 0, 1], [1023, 1023, 1023]])
     assert _cell_keys(c, "morton").tolist() == [4, 2, 1, (1 << 30) - 1]
+
+
+def test_cmake_build_and_ctest(tmp_path):
+    """B01: the CMake build (same flags as _build.py) configures, compiles the gfx950
+    library and the host library, and its CTest host suite passes."""
+    import shutil
+    import subprocess
+
+    if shutil.which("cmake") is None or shutil.which("ninja") is None:
+        pytest.skip("cmake/ninja not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    b = str(tmp_path / "build")
+    for cmd in (["cmake", "-S", root, "-B", b, "-G", "Ninja"],
+                ["cmake", "--build", b, "-j8"],
+                ["ctest", "--test-dir", b, "--output-on-failure"]):
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, f"{' '.join(cmd)} failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    assert os.path.exists(os.path.join(b, "liblsknn_hip.so"))
+    assert os.path.exists(os.path.join(b, "liblsknn_host.so"))
