@@ -168,6 +168,11 @@ __device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int l
     s.bin_hi--;
     s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
   }
+  // bin 0 of a range starting at 0 with shift 0 holds exactly the d² = +0 values: k of
+  // them make the k-th 0 and nothing can be closer — the radius closes (hi_b = 0: every
+  // box and candidate is culled), so k + duplicates of a point cost k candidates, not all
+  // of them (and bin 0's 16-bit counter cannot overflow)
+  if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
 }
 
 // DPP row_newbcast:J — lane J of each 16-lane row to the whole row (folded into the
@@ -786,7 +791,8 @@ __device__ __forceinline__ float bcast64(float v, uint32_t j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
 }
 
-__device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k) {
+__device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k,
+                                                     bool &dup) {
   constexpr int M = 8;
   float best[M];
 #pragma unroll
@@ -805,6 +811,7 @@ __device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nval
       }
     }
   }
+  dup = best[1] == 0.f;  // an exact copy of the query besides itself
   const uint32_t m0 = k < (uint32_t)M ? k : (uint32_t)M;
   float dm = best[0];
 #pragma unroll
@@ -881,7 +888,12 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   W.whx = hx; W.why = hy; W.whz = hz;
 #endif
 
-  float r_est2 = own_group_estimate(s, nvalid, k);
+  bool dup;
+  float r_est2 = own_group_estimate(s, nvalid, k, dup);
+  // an exact copy of the query inside its own group (or k = 1): start with a probe of
+  // the d² = 0 bin (zero probe below) instead of a range around a radius estimate — a
+  // point with >= k copies then costs ~k candidates instead of all its copies
+  const bool zero_est = valid && (dup || r_est2 == 0.f);
   {
     // Robust cap: a group straddling a Morton discontinuity has lanes with few
     // same-side neighbours in the group, whose estimate is then orders of magnitude too
@@ -929,7 +941,16 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       const uint32_t est_b = fbits(r_est2);
       const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;  // top kTopBins/8 oct. above
       const uint32_t lo0 = est_b > off ? est_b - off : 0u;
-      set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
+      if (zero_est) {
+        // zero probe: bins of single float bits from 0 (bin 0 = exact zeros); if fewer
+        // than k values are that small, the overflow resumes at lo0 (band_lo/band_w are
+        // unused while histogramming and carry it)
+        set_range(s, 0u, 0u, s.cut_lim, kUnknown);
+        s.band_lo = lo0;
+        s.band_w = 1u;
+      } else {
+        set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
+      }
     }
   }
 
@@ -980,7 +1001,13 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
           } else {
             ovf = true;
             qs |= QS_OVERFLOW;
-            set_range(s, s.hi_b, kShift0, s.cut_lim, s.c_hi);
+            if (s.band_w != 0u && s.band_lo > s.hi_b) {
+              // failed zero probe: back to the estimate's range (count below it unknown)
+              set_range(s, s.band_lo, kShift0, s.cut_lim, kUnknown);
+            } else {
+              set_range(s, s.hi_b, kShift0, s.cut_lim, s.c_hi);
+            }
+            s.band_lo = s.band_w = 0u;
           }
         } else if (s.bin_hi <= 1 && s.c_base == kUnknown) {
           // k-th in bin 0, which also holds every value below lo_b: the estimate was
