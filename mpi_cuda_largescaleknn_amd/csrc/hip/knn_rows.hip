@@ -890,6 +890,12 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 
   bool dup;
   float r_est2 = own_group_estimate(s, nvalid, k, dup);
+  if (valid && !dup) {
+    // copies sort next to each other: a copy at a group edge may sit in the next group
+    const int64_t nb = lane == 0 ? qi - 1 : (lane == (int)nvalid - 1 ? qi + 1 : -1);
+    if (nb >= 0 && nb < A.nq)
+      dup = A.qpts[3 * nb] == s.qx && A.qpts[3 * nb + 1] == s.qy && A.qpts[3 * nb + 2] == s.qz;
+  }
   // an exact copy of the query inside its own group (or k = 1): start with a probe of
   // the d² = 0 bin (zero probe below) instead of a range around a radius estimate — a
   // point with >= k copies then costs ~k candidates instead of all its copies
