@@ -238,8 +238,9 @@ def test_fused_scatter_keep_d2_and_group_requery():
 
 
 @pytest.mark.parametrize("k", [1, 16, pytest.param(100, marks=pytest.mark.xfail(
-    reason="unique points whose k-th neighbour is one of 60000 equidistant copies: the "
-           "band refinement mis-counts (known limit, docs/ARCHITECTURE.md)", strict=False))])
+    reason="a unique point whose k-th distance shares one 1/8-octave histogram bin with "
+           "> 65535 values (two bases x 60000 copies at similar distance) overflows the "
+           "16-bit bin counter (known limit, docs/ARCHITECTURE.md)", strict=False))])
 def test_knn_heavy_duplicates(k):
     """Points with 60000 exact copies each (all would land in one 16-bit histogram bin
     without the zero probe) next to a sprinkle of unique points: the probe closes the
