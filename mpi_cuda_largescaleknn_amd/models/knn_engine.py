@@ -88,10 +88,57 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None) -> LocalI
     if box is None:
         box = K.bounds(points)
     keys, iota = K.morton(points, box)
-    _, perm = K.sort_pairs(keys, iota, 30)
+    skeys, perm = K.sort_pairs(keys, iota, 30)
+    perm = refine_heavy_cells(points, skeys, perm)
     pts = K.gather3(points, perm, pad=K.PAD_POINTS)
     nodes, qnodes, depth = K.build_tree(pts, n)
     return LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
+
+
+HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key
+
+
+def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    """Order inside over-full key cells (docs/ARCHITECTURE.md §2a).
+
+    Keys have 10 bits per axis of the global cube, so a cluster much smaller than one
+    cell (huge dynamic range, e.g. a dense core in a large box) shares a single key and
+    its buckets all overlap: the k-NN walk cannot cull inside it. When some cell holds
+    more than HEAVY_RUN sorted points, every cell's points are re-keyed on the curve of
+    the cell's own bounding box and the order becomes (cell, local key) — two more
+    stable passes of the same radix sort. Only the order changes (results are exact in
+    any order). Skipped while a HIP graph is being captured (the check needs the host);
+    one compare pass + one host sync otherwise."""
+    n = skeys.shape[0]
+    if n <= HEAVY_RUN:
+        return perm
+    gpu = K.is_gpu(skeys)
+    if gpu and torch.cuda.is_current_stream_capturing():
+        return perm
+    if not bool((skeys[HEAVY_RUN:] == skeys[:-HEAVY_RUN]).any()):
+        return perm
+    dev = skeys.device
+    brk = torch.ones(n, dtype=torch.bool, device=dev)
+    brk[1:] = skeys[1:] != skeys[:-1]
+    rid = torch.cumsum(brk, 0, dtype=torch.int64) - 1
+    nr = int(rid[-1]) + 1
+    p = points[perm.long()]
+    idx3 = rid[:, None].expand(-1, 3)
+    lo = torch.full((nr, 3), math.inf, device=dev).scatter_reduce(0, idx3, p, "amin")
+    hi = torch.full((nr, 3), -math.inf, device=dev).scatter_reduce(0, idx3, p, "amax")
+    ext = hi - lo
+    ext = torch.where(ext > 0, ext, torch.ones_like(ext))
+    q = ((p - lo[rid]) / ext[rid]).clamp_(0.0, 1.0).contiguous()
+    del p, lo, hi, ext
+    # unit cube, scale just under 1024 cells so q = 1 stays in the last cell
+    unit = torch.tensor([0.0, 0.0, 0.0, 1.0, 1.0, 1.0, 1023.5, 1.0], dtype=torch.float32, device=dev)
+    k2, _ = K.morton(q, unit, with_iota=False)
+    del q
+    pos = torch.arange(n, dtype=torch.int32, device=dev)
+    _, o1 = K.sort_pairs(k2, pos, 30)  # by local key ...
+    rbits = max(1, (nr - 1).bit_length())
+    _, o2 = K.sort_pairs(rid.to(torch.int32)[o1.long()], o1, rbits)  # ... then stably by cell
+    return perm[o2.long()].contiguous()
 
 
 def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:

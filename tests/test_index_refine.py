@@ -1,0 +1,48 @@
+"""Second-level keys for over-full key cells (knn_engine.refine_heavy_cells)."""
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from datasets import mixed_scale, uniform  # noqa: E402
+from mpi_cuda_largescaleknn_amd.models import knn_engine as E  # noqa: E402
+from mpi_cuda_largescaleknn_amd.ops import kernels as K  # noqa: E402
+
+
+def _bucket_extent(pts_sorted, sel):
+    """Mean max-axis extent of the 64-point buckets lying entirely inside `sel`."""
+    n = (pts_sorted.shape[0] // 64) * 64
+    b = pts_sorted[:n].view(-1, 64, 3)
+    inside = sel[:n].view(-1, 64).all(1)
+    ext = (b.max(1).values - b.min(1).values).max(1).values
+    return float(ext[inside].mean())
+
+
+def test_sub_cell_cluster_gets_spatial_order(monkeypatch):
+    p = mixed_scale(40000)  # 20000 points in a 1e-3 cube inside a 1000^3 box: one key
+    idx = E.build_index(p)
+    assert torch.equal(torch.sort(idx.perm.long()).values, torch.arange(p.shape[0]))
+    pts = idx.pts[:p.shape[0]]
+    in_cluster = (pts[:, 0] >= 499.99) & (pts[:, 0] <= 500.01)
+    refined = _bucket_extent(pts, in_cluster)
+    monkeypatch.setattr(E, "HEAVY_RUN", 1 << 40)  # refinement off
+    raw = E.build_index(p).pts[:p.shape[0]]
+    plain = _bucket_extent(raw, (raw[:, 0] >= 499.99) & (raw[:, 0] <= 500.01))
+    assert refined < plain / 3, (refined, plain)  # ~1.5x the ideal 64-point cube at this density
+
+
+def test_refined_order_keeps_results_exact():
+    p = mixed_scale(20000, seed=3)
+    for k in (1, 8, 40):
+        got = E.knn_distances(p, k)
+        ref = K.finalize_distances(K.kth_cpu(p, p, k, math.inf))
+        assert torch.equal(got, ref), k
+
+
+def test_uniform_data_is_not_reordered():
+    p = uniform(50000, seed=1)
+    keys, iota = K.morton(p, K.bounds(p))
+    skeys, perm = K.sort_pairs(keys, iota, 30)
+    assert E.refine_heavy_cells(p, skeys, perm) is perm
