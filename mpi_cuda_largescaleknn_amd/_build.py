@@ -62,7 +62,6 @@ def _run(cmd: list[str]) -> None:
 # The SLP vectorizer packs the per-candidate distance math into v_pk_* ops, which cannot
 # take the DPP row broadcast as an operand: it adds a v_mov_dpp per operand and ~50 VGPRs.
 FILE_FLAGS = {
-    "knn.hip": ["-fno-slp-vectorize"],
     # the pass-1 log is a dynamically indexed private array: keep it in scratch memory
     # instead of promoting it to (dynamically indexed, hence many) VGPRs
     "knn_rows.hip": ["-fno-slp-vectorize", "-mllvm", "-disable-promote-alloca-to-vector"],

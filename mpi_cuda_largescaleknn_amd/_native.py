@@ -55,7 +55,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 3  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 4  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -77,6 +77,11 @@ class KnnArgs(C.Structure):
         ("init_d2", vp),
         ("out_perm", vp),
         ("out_final", vp),
+        ("fail_list", vp),
+        ("fail_count", vp),
+        ("fail_cap", i64),
+        ("debug_fail_mod", C.c_int32),
+        ("pad1", C.c_int32),
     ]
 
 
@@ -139,7 +144,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_tree_nodes": ([i64], i64),
         "lsk_hip_build_tree": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_tree_set_radii": ([vp, i64, vp, vp], i32),
-        "lsk_hip_knn": ([C.POINTER(KnnArgs), vp], i32),
+        "lsk_hip_knn_exact": ([C.POINTER(KnnArgs), vp, vp, i64, vp], i32),
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),
         "lsk_hip_flag_query_groups": ([vp, vp, i64, vp, C.c_int32, i64, vp, vp], i32),

@@ -26,6 +26,9 @@ __device__ __forceinline__ cfloat4_p as_const4(const float *p) { return (cfloat4
 __device__ __forceinline__ uint32_t uniform(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
+__device__ __forceinline__ float uniform_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Wave reductions. The result is equal in every lane; the final readfirstlane makes it

@@ -1,0 +1,245 @@
+// Exact k-th-distance backstop: wave-per-query radix select with 32-bit LDS counters.
+//
+// The production kernel (knn_rows.hip) keeps two 16-bit histogram bins per LDS dword and
+// a bounded number of passes: that is what buys its occupancy, and it gives up on a
+// query when a bin would overflow (more than 65535 values in one 1/8-octave bin: massive
+// duplication, a far query looking at a tiny dense cluster), when it runs out of passes
+// or when its collect count disagrees with the histogram. It never emits such a value:
+// it appends the query to a failure list, and this kernel recomputes every listed query
+// exactly, for any input and any k (also k > 65535, which the 16-bit kernel rejects).
+// This is the exactness guarantee of the reference's FlexHeapCandidateList +
+// stackFree::knn (unorderedDataVariant.cu:84-86, 97-102), without its N*k heap memory.
+//
+// Per query (one wave, all control flow wave-uniform):
+//  1. Upper bound: the max d² over k points taken around the query's position in
+//     tree 0 (queries are tree points in curve order, so these are spatial neighbours;
+//     any k distinct points give a valid bound), tightened by init_d2 when given, and
+//     clipped at the -r cutoff.
+//  2. Radix select on the float bits of d² in [lo, hi): every pass walks the bucket
+//     trees (DFS, 8-ary expansion tested by 8 lanes, stack in LDS), prunes boxes whose
+//     distance is >= hi, and counts the values of each 64-point bucket (one point per
+//     lane) into 256 32-bit LDS bins. The bin holding the k-th value becomes the next
+//     [lo, hi); a range of width 1 is the answer. <= 4 counting passes (8 bits each).
+// Same canonical dist² (common.h) as the oracle and the production kernel: bit-identical.
+#include "dev.h"
+
+namespace {
+
+using lsk::bitsf;
+using lsk::fbits;
+
+constexpr int kWaves = 4;  // waves per block
+constexpr int kBins = 256;
+constexpr int kStack = 128;  // DFS stack entries per wave (8-ary: <= 9 * 7 + 1 used)
+
+struct ExactLds {
+  uint32_t hist[kBins];
+  uint32_t stk[kStack];
+};
+
+__device__ __forceinline__ uint32_t cand_bits(float qx, float qy, float qz, const float *p) {
+  return fbits(lsk::dist2(qx - p[0], qy - p[1], qz - p[2]));
+}
+
+// Histogram every value v in [lo, hi) of the points of one tree into hist[(v-lo)>>shift].
+__device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz, uint32_t lo,
+                           uint32_t hi, uint32_t shift, ExactLds &L, int lane) {
+  if (T.n <= 0) return;
+  const int32_t depth = T.depth;
+  const float lim = bitsf(hi);  // a box at distance >= bitsf(hi) holds no value < hi
+  const lsk::vec3f q{qx, qy, qz};
+  const float4 *nodes = (const float4 *)T.nodes;
+  uint32_t sp = 1;
+  if (lane == 0) L.stk[0] = 1u;
+  __builtin_amdgcn_wave_barrier();
+  while (sp > 0) {
+    sp--;
+    const uint32_t node = lsk::uniform(L.stk[sp]);
+    const int32_t lvl = 31 - __clz(node);
+    if (lvl >= depth) {  // a bucket: one point per lane
+      const int64_t b = (int64_t)node - ((int64_t)1 << depth);
+      const int64_t i = b * lsk::kBucket + lane;
+      if (i < T.n) {
+        const uint32_t v = cand_bits(qx, qy, qz, T.pts + 3 * i);
+        if (v >= lo && v < hi) atomicAdd(&L.hist[(v - lo) >> shift], 1u);
+      }
+      continue;
+    }
+    // expand to the descendants `step` levels down (at most the bucket level): lanes
+    // 0..2^step-1 test one box each, the needed ones are pushed
+    const int32_t step = min(3, depth - lvl);
+    const uint32_t nc = 1u << step;
+    const uint32_t child = (node << step) + (uint32_t)lane;
+    bool need = false;
+    if ((uint32_t)lane < nc) {
+      const float4 lo4 = nodes[2 * child], hi4 = nodes[2 * child + 1];
+      need = lsk::box_dist2(q, {lo4.x, lo4.y, lo4.z}, {hi4.x, hi4.y, hi4.z}) < lim;
+    }
+    const uint64_t m = __ballot(need);
+    if (need) {
+      const uint32_t r = __popcll(m & ((1ull << lane) - 1ull));
+      L.stk[sp + r] = child;
+    }
+    sp += (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Upper bound (exclusive, in float bits) of the k-th value: max d² over k points around
+// position `pos` of tree 0 (rest from tree 1 when tree 0 is smaller than k).
+__device__ uint32_t window_bound(const lsk_knn_args &A, int64_t pos, float qx, float qy, float qz,
+                                 uint32_t k, int lane) {
+  const int64_t n0 = A.ntrees > 0 ? A.tree[0].n : 0;
+  const int64_t m0 = n0 < (int64_t)k ? n0 : (int64_t)k;
+  int64_t w0 = pos - (int64_t)(k / 2);
+  if (w0 > n0 - m0) w0 = n0 - m0;
+  if (w0 < 0) w0 = 0;
+  uint32_t vmax = 0;
+  for (int64_t j = lane; j < (int64_t)k; j += lsk::kWave) {
+    const float *p = j < m0 ? A.tree[0].pts + 3 * (w0 + j) : A.tree[1].pts + 3 * (j - m0);
+    vmax = max(vmax, cand_bits(qx, qy, qz, p));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o));
+  return lsk::uniform(vmax);
+}
+
+__device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds &L, int lane) {
+  const uint32_t k = (uint32_t)A.k;
+  const float qx = lsk::uniform_f(A.qpts[3 * qi]);
+  const float qy = lsk::uniform_f(A.qpts[3 * qi + 1]);
+  const float qz = lsk::uniform_f(A.qpts[3 * qi + 2]);
+  const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
+  const uint32_t cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
+  int64_t total = 0;
+  for (int t = 0; t < A.ntrees; t++) total += A.tree[t].n;
+  if (total < (int64_t)k) return cut_b;
+  // 1. upper bound hi (count(< hi) >= k is known when hi_ok)
+  const uint32_t wb = window_bound(A, qi, qx, qy, qz, k, lane);
+  uint32_t hi = cut_lim;
+  bool hi_ok = false;
+  if (wb < cut_lim) {
+    hi = wb + 1u;
+    hi_ok = true;
+  }
+  if (A.init_d2) {
+    const float ub = A.init_d2[qi];
+    if (ub >= 0.f && ub < __builtin_inff() && fbits(ub) + 1u < hi) {
+      hi = fbits(ub) + 1u;
+      hi_ok = true;
+    }
+  }
+  // 2. radix select on [lo, hi)
+  uint32_t lo = 0, below = 0;  // below = count of values < lo
+  for (int pass = 0; pass < 8; pass++) {
+    const uint32_t width = hi - lo;
+    if (hi_ok && width == 1u) return lo;
+    if (width == 0u) return cut_b;  // (not reached: hi > lo always holds)
+    uint32_t shift = 0;
+    while (((width - 1u) >> shift) >= (uint32_t)kBins) shift++;
+#pragma unroll
+    for (int j = 0; j < kBins / lsk::kWave; j++) L.hist[j * lsk::kWave + lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    for (int t = 0; t < A.ntrees; t++) count_tree(A.tree[t], qx, qy, qz, lo, hi, shift, L, lane);
+    __builtin_amdgcn_wave_barrier();
+    // lane l owns bins 4l .. 4l+3
+    const uint32_t c0 = L.hist[4 * lane], c1 = L.hist[4 * lane + 1];
+    const uint32_t c2 = L.hist[4 * lane + 2], c3 = L.hist[4 * lane + 3];
+    const uint32_t s = c0 + c1 + c2 + c3;
+    uint32_t incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+      if (lane >= o) incl += y;
+    }
+    const uint32_t sum = lsk::uniform((uint32_t)__shfl((int)incl, 63));
+    if ((uint64_t)below + sum < (uint64_t)k) return cut_b;  // < k values below the cutoff
+    const uint32_t need = k - below;
+    const uint32_t excl = incl - s;
+    const bool mine = excl < need && incl >= need;
+    const int src = (int)__builtin_ctzll(__ballot(mine));
+    // bin inside the owning lane and the count below it
+    uint32_t bsel = 3u, before = excl + c0 + c1 + c2;
+    if (excl + c0 >= need) {
+      bsel = 0u;
+      before = excl;
+    } else if (excl + c0 + c1 >= need) {
+      bsel = 1u;
+      before = excl + c0;
+    } else if (excl + c0 + c1 + c2 >= need) {
+      bsel = 2u;
+      before = excl + c0 + c1;
+    }
+    const uint32_t b = 4u * (uint32_t)src + (uint32_t)__shfl((int)bsel, src);
+    below += (uint32_t)__shfl((int)before, src);
+    below = lsk::uniform(below);
+    const uint32_t nlo = lo + (lsk::uniform(b) << shift);
+    const uint64_t nhi = (uint64_t)nlo + (1ull << shift);
+    hi = nhi < (uint64_t)hi ? (uint32_t)nhi : hi;
+    lo = nlo;
+    hi_ok = true;
+  }
+  return 0x7fc00000u;  // unreachable: width shrinks 256x per pass
+}
+
+__global__ __launch_bounds__(kWaves * 64) void knn_exact_kernel(const lsk_knn_args A,
+                                                                const uint32_t *__restrict__ list,
+                                                                const uint32_t *__restrict__ count,
+                                                                int64_t cap) {
+  __shared__ ExactLds lds[kWaves];
+  const int wid = threadIdx.x >> 6;
+  const int lane = lsk::lane_id();
+  ExactLds &L = lds[wid];
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + wid;
+  const int64_t tw = (int64_t)gridDim.x * kWaves;
+  int64_t total;
+  if (list) {
+    const int64_t c = (int64_t)count[0];
+    total = c < cap ? c : cap;
+  } else {
+    total = A.groups ? A.ngroups * lsk::kBucket : A.nq;
+  }
+  for (int64_t i = gw; i < total; i += tw) {
+    int64_t qi;
+    if (list) {
+      qi = (int64_t)list[i];
+    } else if (A.groups) {
+      qi = (int64_t)A.groups[i / lsk::kBucket] * lsk::kBucket + (i % lsk::kBucket);
+    } else {
+      qi = i;
+    }
+    qi = (int64_t)lsk::uniform((uint32_t)qi);
+    if (qi >= A.nq) continue;
+    const uint32_t ans = exact_kth(A, qi, L, lane);
+    if (lane == 0) {
+      if (A.out_d2) A.out_d2[qi] = bitsf(ans);
+      if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(ans));
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lsk_hip_knn_exact(const lsk_knn_args *args, const uint32_t *list,
+                                 const uint32_t *count, int64_t cap, void *stream) {
+  const lsk_knn_args &A = *args;
+  if (A.k < 1 || A.nq >= ((int64_t)1 << 32) || A.ntrees < 0 || A.ntrees > 2) {
+    lsk::set_last_error("knn_exact: k >= 1, nq < 2^32, ntrees in [0,2]");
+    return 1;
+  }
+  for (int t = 0; t < A.ntrees; t++) {
+    if (A.tree[t].depth > 30 || !A.tree[t].nodes || !A.tree[t].pts) {
+      lsk::set_last_error("knn_exact: tree view incomplete");
+      return 1;
+    }
+  }
+  if (list && (!count || cap <= 0)) return 0;
+  const int64_t work = list ? cap : (A.groups ? A.ngroups * lsk::kBucket : A.nq);
+  if (work <= 0) return 0;
+  // persistent grid-stride loop: 2048 blocks x 4 waves (every wave exits at the end of
+  // the list; with an empty failure list the launch is a few microseconds)
+  const unsigned nblk = lsk_blocks(work, kWaves, 2048);
+  knn_exact_kernel<<<nblk, kWaves * 64, 0, (hipStream_t)stream>>>(A, list, count, cap);
+  LSK_CHECK_LAUNCH("knn_exact");
+  return 0;
+}

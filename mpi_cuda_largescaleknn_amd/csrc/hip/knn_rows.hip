@@ -822,8 +822,26 @@ __device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nval
 enum : uint32_t {
   QS_OVERFLOW = 1, QS_UNDERFLOW = 2, QS_REFINE = 4, QS_LIST_INVALID = 8, QS_COLLECTED = 16,
   QS_DONE_BAND1 = 32, QS_DONE_CUT = 64, QS_DONE_ZERO = 128, QS_LIMIT = 256, QS_MISMATCH = 512,
-  QS_HINT = 1024
+  QS_HINT = 1024, QS_BINOVF = 2048,
+  QS_FAIL = 4096  // not resolved here: NaN placeholder + failure list (knn_exact.hip)
 };
+constexpr uint32_t kNaNBits = 0x7fc00000u;
+
+// 16-bit bin checksum of a lane's histogram: c_hi (a 32-bit register) is exactly the
+// number of counted values in bins [0, bin_hi), and every wrap of a 16-bit counter
+// (an even bin carrying into its odd neighbour, an odd bin carrying out of the dword)
+// changes the sum of the counters by -65535 or -65536 — so the sum equals c_hi iff no
+// bin overflowed during the pass (values of dropped top bins were subtracted from c_hi
+// as read, which preserves the identity).
+__device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *pool, int lane) {
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kBins / 2; j++) {
+    const uint32_t w = pool[j * lsk::kWave + lane];
+    sum += (2 * j < s.bin_hi ? (w & 0xffffu) : 0u) + (2 * j + 1 < s.bin_hi ? (w >> 16) : 0u);
+  }
+  return sum == s.c_hi;
+}
 
 template <int RCAP, int NT>
 __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_rows_kernel(const lsk_knn_args A) {
@@ -969,11 +987,13 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   for (;;) {
     while (__ballot(s.state == ST_HIST)) {
       if (++passes > kMaxPasses) {
+        // every unresolved lane (histogramming or waiting for the collect) goes to the
+        // exact backstop
         limit = 1;
-        if (s.state == ST_HIST) {
+        if (s.state != ST_DONE) {
           s.state = ST_DONE;
-          s.ans = 0x7fc00000u;
-          qs |= QS_LIMIT;
+          s.ans = kNaNBits;
+          qs |= QS_LIMIT | QS_FAIL;
         }
         break;
       }
@@ -997,6 +1017,11 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       W.logging = false;
       first = false;
       bool ovf = false;
+      if (s.state == ST_HIST && !hist_consistent(s, W.L->pool, lane)) {
+        s.state = ST_DONE;  // a 16-bit bin wrapped: counts are unusable
+        s.ans = kNaNBits;
+        qs |= QS_BINOVF | QS_FAIL;
+      }
       if (s.state == ST_HIST) {
         const uint32_t top = top_count(s, W.L->pool, lane);
         if (s.c_hi < k) {
@@ -1083,10 +1108,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     LSK_PT(ts0);
     if (s.state == ST_READY) {
       qs |= QS_COLLECTED;
-      if (s.ccnt != s.bc) qs |= QS_MISMATCH;
+      if (s.ccnt != s.bc) qs |= QS_MISMATCH | QS_FAIL;
       uint32_t *h = W.L->pool + s.coff;
       const uint32_t c = min(s.ccnt, s.bc), m = s.m;
-      if (m >= 1 && m <= c) {
+      if (!(qs & QS_FAIL) && m >= 1 && m <= c) {
         for (int i = (int)(m / 2) - 1; i >= 0; i--) heap_sift(h, (uint32_t)i, m);
         for (uint32_t i = m; i < c; i++) {
           const uint32_t v = h[i];
@@ -1097,11 +1122,28 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
         }
         s.ans = h[0];
       } else {
-        qs |= QS_MISMATCH;
-        s.ans = 0x7fc00000u;
+        qs |= QS_MISMATCH | QS_FAIL;
+        s.ans = kNaNBits;
       }
     }
     LSK_PADD(W.prof[6], ts0);
+  }
+
+  // a truncated walk (watchdog) invalidates the whole wave; tests can force failures
+  if (W.guard) qs |= QS_FAIL;
+  if (A.debug_fail_mod > 0 && qi % A.debug_fail_mod == 0) qs |= QS_FAIL;
+  const bool failed = valid && (qs & QS_FAIL);
+  if (failed) s.ans = kNaNBits;
+  if (A.fail_count) {
+    // failure list: one atomic per wave with failures, lanes write their slots
+    const uint64_t fm = __ballot(failed);
+    if (fm) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(A.fail_count, (uint32_t)__popcll(fm));
+      base = lsk::uniform(base);
+      const uint64_t slot = (uint64_t)base + (uint64_t)__popcll(fm & ((1ull << lane) - 1ull));
+      if (failed && slot < (uint64_t)A.fail_cap) A.fail_list[slot] = (uint32_t)qi;
+    }
   }
 
   if (valid) {
@@ -1129,7 +1171,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       return (unsigned long long)__popcll(__ballot(valid && (qs & bit)));
     };
     const unsigned long long c_ovf = cnt(QS_OVERFLOW), c_udf = cnt(QS_UNDERFLOW),
-                             c_ref = cnt(QS_REFINE), c_mm = cnt(QS_MISMATCH), c_hint = cnt(QS_HINT);
+                             c_ref = cnt(QS_REFINE), c_mm = cnt(QS_MISMATCH), c_hint = cnt(QS_HINT),
+                             c_fail = cnt(QS_FAIL), c_bovf = cnt(QS_BINOVF);
     if (lane == 0) {
       atomicAdd(&A.stats[0], (unsigned long long)W.steps * 16ull);  // candidates per lane
       atomicAdd(&A.stats[1], (unsigned long long)W.quarters);
@@ -1147,6 +1190,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       atomicAdd(&A.stats[13], (unsigned long long)W.csteps);
       atomicAdd(&A.stats[14], (unsigned long long)W.cnodes);
       atomicAdd(&A.stats[15], (unsigned long long)W.guard);
+      atomicAdd(&A.stats[26], c_fail);
+      atomicAdd(&A.stats[27], c_bovf);
     }
   }
 }

@@ -108,10 +108,23 @@ typedef struct lsk_knn_args {
   const uint32_t *out_perm; // optional fused result scatter: when set, the kernel also
   float *out_final;         // writes out_final[out_perm[q]] = sqrtf(d2) (inf stays inf),
                             // which saves a separate scatter kernel
+  uint32_t *fail_list;      // failure list of the 16-bit kernel (knn_rows): sorted-order
+  uint32_t *fail_count;     // query indices it could not resolve exactly, and their count
+  int64_t fail_cap;         // (the count may exceed the capacity: then the host reruns all)
+  int32_t debug_fail_mod;   // tests only: also fail every query qi with qi % mod == 0
+  int32_t pad1;
 } lsk_knn_args;
 
-int lsk_hip_knn(const lsk_knn_args *args, void *stream);       // 64-query group kernel
-int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream);  // 4 x 16-query rows (default)
+// Production kernel: 4 x 16-query rows, 16-bit LDS histogram radix select. Queries it
+// cannot resolve exactly (bin overflow, pass limit, collect mismatch, walk guard) get a
+// NaN placeholder and are appended to fail_list (fail_count is the always-on failure word).
+int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream);
+// Exact backstop for any input and any k >= 1: wave per query, 32-bit bins. list != NULL:
+// the queries list[0 .. min(*count, cap)) (count is read on the device: graph-capturable,
+// an empty list costs one short launch); list == NULL: every query (or every query of
+// args->groups).
+int lsk_hip_knn_exact(const lsk_knn_args *args, const uint32_t *list, const uint32_t *count,
+                      int64_t cap, void *stream);
 
 // ---- halo exchange -------------------------------------------------------------------
 // Published tree: the top `levels` levels of a tree (node slots 1 .. 2^levels-1... up to

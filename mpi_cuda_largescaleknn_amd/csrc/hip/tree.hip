@@ -105,6 +105,9 @@ __global__ __launch_bounds__(256) void leaf_radius_kernel(const float *__restric
   if (leaf >= nleaf_slots) return;
   const int64_t i = leaf * lsk::kBucket + lsk::lane_id();
   float r = i < n ? d2[i] : 0.f;
+  // an unresolved (NaN) radius must widen the published halo bound, never vanish in
+  // fmaxf: treat it as +inf (the exact backstop normally replaces every NaN first)
+  r = r == r ? r : __builtin_inff();
   r = rows_max(max16(r));
   if (lsk::lane_id() == 0) nodes[8 * (((int64_t)1 << depth) + leaf) + 3] = r;
 }

@@ -30,7 +30,11 @@ def cut2_of(max_radius: float) -> float:
 
 
 SEED_BUCKETS = 2  # Morton-neighbour buckets (each side) that seed the first pass
-KNN_IMPL = "rows"  # "rows" (4 x 16-query rows, quarter culling) or "wave" (64-query groups)
+KNN_IMPL = "rows"  # "rows" (production kernel + exact backstop) or "exact" (backstop only)
+DEBUG_FAIL_MOD = 0  # tests: make the rows kernel hand every m-th query to the backstop
+# HIP-graph captures: the failure words of captured launches, checked after a replay
+# (verify_captured_failures) — during a capture the host cannot read them
+CAPTURED_FAIL_WORDS: list = []
 
 
 @dataclass
@@ -74,10 +78,13 @@ class KnnStats:
                  # cycle profile (LSK_PROFILE kernel builds only)
                  "prof_proc_hist", "prof_proc_collect", "prof_walk_hist", "prof_walk_collect",
                  "prof_quarters", "prof_inner_nodes", "prof_select", "prof_wave",
-                 "prof_rows_entry", "prof_rows_in"]
+                 "prof_rows_entry", "prof_rows_in", "failed_lanes", "binovf_lanes"]
         vals = raw.cpu().tolist()
         for i, nm in enumerate(names):
             self.counters[nm] = self.counters.get(nm, 0) + int(vals[i])
+
+    def add_fallback(self, n: int) -> None:
+        self.counters["fallback_queries"] = self.counters.get("fallback_queries", 0) + int(n)
 
 
 def build_index(points: torch.Tensor, box: torch.Tensor | None = None) -> LocalIndex:
@@ -207,12 +214,38 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
         return out if want_d2 else final_out
     trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
     raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
-    K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, groups=groups, ngroups=ngroups,
-              stats=raw, qstatus=qstatus, seed=SEED_BUCKETS, impl=KNN_IMPL, init_d2=init_d2,
+    kw = dict(groups=groups, ngroups=ngroups, seed=SEED_BUCKETS, init_d2=init_d2,
               out_perm=index.perm if final_out is not None else None, out_final=final_out)
+    fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
+                   impl=KNN_IMPL, debug_fail_mod=DEBUG_FAIL_MOD, **kw)
+    if torch.cuda.is_current_stream_capturing():
+        CAPTURED_FAIL_WORDS.append(fw)
+    elif fw.count is not None:
+        # one 4-byte read: failures beyond the list capacity (pathological input) rerun
+        # the whole query on the exact kernel
+        nfail = fw.value()
+        if nfail > fw.cap:
+            K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", **kw)
+        if stats is not None:
+            stats.add_fallback(nfail)
     if stats is not None:
         stats.add(raw)
     return out if want_d2 else final_out
+
+
+def verify_captured_failures(clear: bool = False) -> int:
+    """After replaying a captured graph: total backstop queries of the captured launches;
+    raises if one overflowed its failure list (the graph's output is then incomplete)."""
+    total = 0
+    for fw in CAPTURED_FAIL_WORDS:
+        v = fw.value()
+        if v > fw.cap:
+            raise RuntimeError(f"k-NN failure list overflow in a captured graph ({v} > {fw.cap}): "
+                               "rerun eagerly")
+        total += v
+    if clear:
+        CAPTURED_FAIL_WORDS.clear()
+    return total
 
 
 def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,

@@ -217,27 +217,60 @@ def radius_hint(box: torch.Tensor, n_total: int, k: int) -> torch.Tensor:
     return out
 
 
+ROWS_MAX_K = 65535  # 16-bit histogram bins of knn_rows; larger k go to the exact kernel
+
+
+def fail_capacity(work: int) -> int:
+    """Capacity of the failure list of one knn_rows launch over `work` queries: all of
+    them up to 64M, then 1/16 of them (a failure count above it makes the host rerun the
+    whole query on the exact kernel, see knn_engine.query)."""
+    return max(1, min(work, max(1 << 26, work >> 4)))
+
+
+class FailWord:
+    """Always-on failure word of one k-NN launch: count (device int32) of the queries the
+    16-bit kernel handed to the exact backstop, and the list capacity. Reading it syncs."""
+
+    def __init__(self, count: torch.Tensor | None, cap: int):
+        self.count = count
+        self.cap = cap
+
+    def value(self) -> int:
+        return 0 if self.count is None else int(self.count.item())
+
+    def overflowed(self) -> bool:
+        return self.value() > self.cap
+
+
 def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             r_hint2: float | torch.Tensor,
             out_d2: torch.Tensor, groups: torch.Tensor | None = None, ngroups: int = 0,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
-            out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None) -> torch.Tensor:
+            out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
+            debug_fail_mod: int = 0) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
-    trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (4 x 16-query
-    rows with per-row quarter culling, default) or "wave" (64-query groups). seed > 0 declares that the
-    queries are trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
+    trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
+    production kernel: 4 x 16-query rows, 16-bit LDS histograms; every query it cannot
+    resolve exactly goes to the failure list and is recomputed by the exact kernel in the
+    same stream, no host round trip) or "exact" (the wave-per-query 32-bit backstop for
+    every query; also used for k > 65535). seed > 0 declares that the queries are
+    trees[0]'s points in tree order (pass 1 starts from neighbour buckets).
     init_d2 (optional, [nq]): a known upper bound of every query's k-th squared distance
     (e.g. the local result before a halo re-query) that places the first range.
-    out_perm / out_final (optional, fused scatter): the kernel also writes
+    out_perm / out_final (optional, fused scatter): the kernels also write
     out_final[out_perm[q]] = final distance; out_d2 may then be None.
+    debug_fail_mod (tests): the rows kernel also fails every query q with q % mod == 0.
+    Returns the launch's FailWord.
     """
     if (out_perm is None) != (out_final is None):
         raise ValueError("knn_gpu: out_perm and out_final go together")
     if out_perm is not None and (out_perm.shape[0] < nq or out_perm.dtype != torch.int32
                                  or not out_perm.is_contiguous() or out_final.dtype != torch.float32):
         raise ValueError("knn_gpu: out_perm must be int32 [>= nq], out_final float32")
+    if impl not in ("rows", "exact"):
+        raise ValueError(f"knn_gpu: impl must be rows or exact, not {impl!r}")
     a = KnnArgs()
     a.qpts = _ptr(qpts)
     a.nq = nq
@@ -262,10 +295,23 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.init_d2 = _ptr(init_d2)
     a.out_perm = _ptr(out_perm)
     a.out_final = _ptr(out_final)
+    a.debug_fail_mod = int(debug_fail_mod)
     lib = _native.hip()
-    fn = lib.lsk_hip_knn_rows if impl == "rows" else lib.lsk_hip_knn
-    check(fn(C.byref(a), _stream(qpts)), "knn")
-    return out_d2
+    st = _stream(qpts)
+    if impl == "exact" or k > ROWS_MAX_K:
+        check(lib.lsk_hip_knn_exact(C.byref(a), None, None, 0, st), "knn_exact")
+        return FailWord(None, 0)
+    work = ngroups * BUCKET if groups is not None else nq
+    cap = fail_capacity(work)
+    count = torch.zeros(1, dtype=torch.int32, device=qpts.device)
+    flist = torch.empty(cap, dtype=torch.int32, device=qpts.device)
+    a.fail_list = _ptr(flist)
+    a.fail_count = _ptr(count)
+    a.fail_cap = cap
+    check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
+    # exact backstop over the failure list (device-side count: empty list = short no-op)
+    check(lib.lsk_hip_knn_exact(C.byref(a), _ptr(flist), _ptr(count), cap, st), "knn_exact")
+    return FailWord(count, cap)
 
 
 def kth_cpu(points: torch.Tensor, queries: torch.Tensor, k: int, cut2: float, method: str = "kdtree") -> torch.Tensor:
