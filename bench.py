@@ -4,13 +4,19 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--points P] [--k K] [--variant V]
 
 Launched by the driver as ``torch.distributed.run --nproc-per-node N bench.py --gpus N``
-for N > 1 (one rank per GPU, RCCL over xGMI). Each rank owns the reference's
-block partition [floor(P*r/N), floor(P*(r+1)/N)) of one global synthetic uniform-random
-point set held in pinned host memory. One timed step = the BASELINE.md clock: host
-points -> H2D -> (unordered variant) spatial redistribution + bucket-tree k-NN + halo
-exchange + result return -> distances back in host memory. W untimed warmup steps, then
-K steps bracketed by barrier + device sync; the max over ranks is reported.
-Rank 0 prints one JSON line.
+for N > 1 (one rank per GPU, RCCL over xGMI; bootstrap through parallel/launch.init:
+NUMA binding, collective timeout, watchdog, abort broadcast). Each rank owns the
+reference's block partition [floor(P*r/N), floor(P*(r+1)/N)) of ONE global synthetic
+uniform-random point set held in pinned host memory: the set is generated in chunks of
+2^24 points seeded by the chunk's global index, so it is the same for every N and the
+outputs at N = 1/2/4/8 are comparable bit for bit. One timed step = the BASELINE.md
+clock: host points -> H2D -> (unordered variant) spatial redistribution + bucket-tree
+k-NN + halo exchange + result return -> distances back in host memory. W untimed warmup
+steps, then K steps bracketed by barrier + device sync; the max over ranks is reported.
+
+After the timed region (untimed): one instrumented step (per-phase times, max over
+ranks; halo sizes; per-rank k-NN ms) and a brute-force check of 256 sampled outputs
+against all points (utils/verify.py, `sampled_exact`). Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -22,18 +28,30 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from mpi_cuda_largescaleknn_amd.models import knn_engine as E  # noqa: E402
 from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
-from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm  # noqa: E402
-from mpi_cuda_largescaleknn_amd.utils import numa, trace  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel import launch as LA  # noqa: E402
+from mpi_cuda_largescaleknn_amd.utils import trace, verify  # noqa: E402
 
-METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
+HEADLINE_METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
+GEN_CHUNK = 1 << 24  # points per seeded generation chunk (global index -> seed)
+PHASES = ["bounds", "partition", "alltoallv_points", "build", "knn_local", "halo_publish",
+          "halo_filter", "halo_alltoallv", "halo_tree", "halo_requery", "return"]
+COUNTS = ["sent_points", "owned_points", "halo_sent", "halo_recv", "requery_groups"]
+
+
+def metric_name(n_total: int, k: int) -> str:
+    """The BASELINE.json metric for the headline config; the label follows --points/--k."""
+    if n_total == 10**9 and k == 100:
+        return HEADLINE_METRIC
+    pts = f"{n_total / 1e9:g}B" if n_total >= 10**9 else f"{n_total / 1e6:g}M"
+    return f"Mpoints/sec kNN-distance (k={k}) on {pts} float3 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # BASELINE.md: the reference publishes no numbers
 
 
@@ -61,25 +79,37 @@ def parse():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = rehearsal of the launch/timing contract (gloo, CPU oracle); "
                          "never a measurement")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="multi-rank pipeline and RCCL collectives even on one rank")
+    ap.add_argument("--verify", type=int, default=256,
+                    help="sampled outputs checked by brute force after the timed region (0 = off)")
     return ap.parse_args()
 
 
+def block_range(n_total: int, rank: int, size: int) -> tuple[int, int]:
+    """The reference's readFilePortion partition (unorderedDataVariant.cu:42-63)."""
+    return n_total * rank // size, n_total * (rank + 1) // size
+
+
 def make_points(n_total: int, rank: int, size: int, device, variant: str) -> torch.Tensor:
-    """This rank's slice of the global synthetic set, in pinned host memory."""
-    b = n_total * rank // size
-    e = n_total * (rank + 1) // size
-    n = e - b
-    g = torch.Generator(device=device)
-    g.manual_seed(1234 + rank)
-    host = torch.empty((n, 3), dtype=torch.float32, pin_memory=device.type == "cuda")
-    chunk = 1 << 26
-    for s in range(0, n, chunk):
-        m = min(chunk, n - s)
-        d = torch.rand((m, 3), generator=g, device=device, dtype=torch.float32)
-        if variant == "prepartitioned":
-            # spatially tiled files: rank r owns the slab [r/size, (r+1)/size) in x
-            d[:, 0] = (d[:, 0] + rank) / size
-        host[s:s + m].copy_(d)
+    """This rank's block of the global synthetic set, in pinned host memory. Chunk c of
+    the global set (GEN_CHUNK points) always comes from seed 1234 + c, so the global set
+    does not depend on the rank count (per device type)."""
+    b, e = block_range(n_total, rank, size)
+    host = torch.empty((e - b, 3), dtype=torch.float32, pin_memory=device.type == "cuda")
+    if e > b:
+        for c in range(b // GEN_CHUNK, (e - 1) // GEN_CHUNK + 1):
+            c0 = c * GEN_CHUNK
+            g = torch.Generator(device=device)
+            g.manual_seed(1234 + c)
+            d = torch.rand((min(GEN_CHUNK, n_total - c0), 3), generator=g, device=device,
+                           dtype=torch.float32)
+            lo, hi = max(b, c0), min(e, c0 + GEN_CHUNK)
+            part = d[lo - c0:hi - c0]
+            if variant == "prepartitioned":
+                # spatially tiled files: rank r owns the slab [r/size, (r+1)/size) in x
+                part[:, 0] = (part[:, 0] + rank) / size
+            host[lo - b:hi - b].copy_(part)
     _sync(device)
     return host
 
@@ -91,29 +121,16 @@ def _sync(device):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.device == "cuda":
-        # one rank per GPU (ranks beyond the device count wrap: rehearsals with
-        # LSKNN_DIST_BACKEND=gloo only, RCCL refuses two ranks on one GPU)
-        dev_id = local_rank % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev_id)
-        device = torch.device("cuda", dev_id)
-        # host side (pinned input/output buffers) on the GPU's NUMA node
-        bound = numa.bind_to_device(device)
-        if bound and args.phases:
-            print(f"rank {rank}: bound to {bound}", file=sys.stderr)
-    else:
-        device = torch.device("cpu")
-    if world > 1:
-        if device.type == "cuda" and os.environ.get("LSKNN_DIST_BACKEND", "nccl") == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group("gloo")
-        comm = TorchComm(device)
-    else:
-        comm = SingleComm(device)
+    # a hung collective ends the job (watchdog + collective timeout) long before the
+    # driver's limit; one rank per GPU (ranks beyond the device count wrap: rehearsals
+    # with LSKNN_DIST_BACKEND=gloo only, RCCL refuses two ranks on one GPU); pinned
+    # buffers on the GPU's NUMA node
+    os.environ.setdefault("LSKNN_TIMEOUT", "600")
+    launch = LA.init(device_pref=args.device, force_distributed=args.force_dist or None,
+                     verbose=args.phases)
+    world, rank, device, comm = launch.size, launch.rank, launch.device, launch.comm
+    if args.device == "cuda" and device.type != "cuda":
+        raise RuntimeError("bench.py: no GPU available (use --device cpu for a rehearsal)")
     n_total = int(args.points)
     cfg = KnnConfig(k=args.k, collect_stats=args.stats)
 
@@ -122,16 +139,16 @@ def main():
 
     info_last = None
     direct = (PL.direct_host_out_pays(args.k) if args.direct_out < 0 else bool(args.direct_out)) \
-        and world == 1 and device.type == "cuda"
+        and not comm.distributed and device.type == "cuda"
 
     def step():
         with trace.range("lsknn:step"):
             _step()
             _sync(device)
 
-    def _step():
+    def _step(phases: bool = args.phases):
         nonlocal info_last
-        info = PL.RunInfo(PL.PhaseTimer(args.phases, device))
+        info = PL.RunInfo(PL.PhaseTimer(phases, device))
         pts = host_pts.to(device, non_blocking=True)
         if args.mode == "ring":
             out = RA.ring_knn(pts, comm, cfg, info)
@@ -147,7 +164,7 @@ def main():
         info_last = info
 
     use_graph = (args.graph == 1 or (args.graph < 0 and not (args.phases or args.stats))) \
-        and world == 1 and device.type == "cuda" and args.mode == "halo"
+        and not comm.distributed and device.type == "cuda" and args.mode == "halo"
     graph = None
     if use_graph:
         # warm up on a side stream (allocator + library state), then capture one whole
@@ -187,14 +204,25 @@ def main():
 
     ms = elapsed / args.steps * 1e3
     value = n_total * args.steps / elapsed / 1e6
-    # sanity: distances must be finite and positive for uniform data with k <= n
-    finite = bool(torch.isfinite(host_out).all()) if host_out.numel() else True
+    if graph is not None:
+        E.verify_captured_failures(clear=True)  # raises if a replay overflowed a failure list
+    finite_t = torch.tensor([0 if host_out.numel() == 0 or bool(torch.isfinite(host_out).all()) else 1],
+                            dtype=torch.int64, device=device)
+    comm.allreduce_(finite_t, "sum")
+    finite = int(finite_t.item()) == 0
+
+    # ---- untimed: sampled brute-force check of the timed result, then one instrumented step
+    check = None
+    if args.verify > 0 and args.variant == "unordered":
+        b, _ = block_range(n_total, rank, world)
+        check = verify.sampled_exact(comm, host_pts, host_out, b, n_total, args.k, args.verify)
+    detail = instrumented_detail(comm, lambda: (_step(phases=True), _sync(device)), lambda: info_last)
     if rank == 0:
         if args.phases or args.stats:
             print(json.dumps({"phases_s": info_last.timer.times, "counts": info_last.counts,
                               "knn_stats": info_last.stats.counters}), file=sys.stderr)
         rec = {
-            "metric": METRIC,
+            "metric": metric_name(n_total, args.k),
             "value": round(value, 3),
             "unit": "Mpoints/s",
             "n_gpus": world,
@@ -216,11 +244,38 @@ def main():
                 "k": args.k,
                 "hip_graph": graph is not None,
                 "all_finite": finite,
+                "sampled_exact": (f"{check['exact']}/{check['samples']}" if check else None),
             },
+            "detail": dict(detail, sampled_exact=check),
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    LA.finalize(launch)
+
+
+def instrumented_detail(comm, run_step, last_info) -> dict:
+    """One extra untimed step with device-synchronised phase marks; returns the max over
+    ranks of every phase time, per-rank k-NN and step ms, and the summed exchange sizes."""
+    t0 = time.perf_counter()
+    run_step()
+    step_s = time.perf_counter() - t0
+    info = last_info()
+    vec = [info.timer.times.get(p, 0.0) for p in PHASES] + [step_s] + \
+        [float(info.counts.get(c, 0)) for c in COUNTS]
+    allv = comm.allgather(torch.tensor(vec, dtype=torch.float64, device=comm.device)).cpu()
+    np_ = len(PHASES)
+    phases_max = {p: round(float(allv[:, i].max()) * 1e3, 3) for i, p in enumerate(PHASES)
+                  if float(allv[:, i].max()) > 0}
+    counts_sum = {c: int(allv[:, np_ + 1 + i].sum()) for i, c in enumerate(COUNTS)}
+    return {
+        "phase_ms_max_over_ranks": phases_max,
+        "instrumented_step_ms_per_rank": [round(float(x) * 1e3, 3) for x in allv[:, np_]],
+        "knn_local_ms_per_rank": [round(float(x) * 1e3, 3) for x in allv[:, PHASES.index("knn_local")]],
+        "halo_requery_ms_per_rank": [round(float(x) * 1e3, 3) for x in allv[:, PHASES.index("halo_requery")]],
+        "redistributed_bytes": counts_sum["sent_points"] * 12,
+        "halo_bytes": counts_sum["halo_sent"] * 12,
+        "requery_groups": counts_sum["requery_groups"],
+        "owned_points_per_rank": [int(x) for x in allv[:, np_ + 1 + COUNTS.index("owned_points")]],
+    }
 
 
 if __name__ == "__main__":

@@ -107,6 +107,8 @@ def _declare_host(lib: C.CDLL) -> None:
         f = getattr(lib, name)
         f.argtypes = [vp, i64, vp, i64, i32, C.c_float, vp, i32]
         f.restype = None
+    lib.lsk_cpu_count_below.argtypes = [vp, i64, vp, vp, i32, vp, i32]
+    lib.lsk_cpu_count_below.restype = None
     lib.lsk_cpu_bounds.argtypes = [vp, i64, vp, i32]
     lib.lsk_cpu_bounds.restype = None
     lib.lsk_cpu_morton.argtypes = [vp, i64, vp, C.c_float, vp, i32, i32]
@@ -157,6 +159,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_gather_u32": ([vp, vp, i64, vp, vp], i32),
         "lsk_hip_refalgo_knn": ([vp, i64, vp, i64, vp, i32, C.c_float, i32, vp, C.c_uint32, vp], i32),
         "lsk_hip_refalgo_extract": ([vp, i64, i32, vp, vp], i32),
+        "lsk_hip_count_below": ([vp, i64, vp, vp, i32, vp, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

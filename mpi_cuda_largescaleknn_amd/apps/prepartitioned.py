@@ -56,7 +56,7 @@ def _run(args, launch, names) -> int:
         # one GPU rank, large k: the k-NN kernel writes the distances straight into
         # pinned host memory (PL.direct_host_out_pays)
         host_out = (torch.empty(pts.shape[0], dtype=torch.float32, pin_memory=True)
-                    if launch.device.type == "cuda" and launch.size == 1
+                    if launch.device.type == "cuda" and not launch.comm.distributed
                     and PL.direct_host_out_pays(cfg.k) else None)
         out = PL.prepartitioned_knn(dpts, launch.comm, cfg, info, out=host_out)
     res = out.cpu()

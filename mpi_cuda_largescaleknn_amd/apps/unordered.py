@@ -47,7 +47,7 @@ def _run(args, launch) -> int:
         # one GPU rank, large k: the k-NN kernel writes the distances straight into
         # pinned host memory (PL.direct_host_out_pays)
         host_out = (torch.empty(pts.shape[0], dtype=torch.float32, pin_memory=True)
-                    if launch.device.type == "cuda" and launch.size == 1
+                    if launch.device.type == "cuda" and not launch.comm.distributed
                     and PL.direct_host_out_pays(cfg.k) else None)
         out = PL.unordered_knn(dpts, launch.comm, cfg, info, n_total=total, out=host_out)
     res = out.cpu()

@@ -170,6 +170,12 @@ int lsk_hip_refalgo_knn(const float *tree, int64_t n, const float *qpts, int64_t
 int lsk_hip_refalgo_extract(const unsigned long long *heaps, int64_t nq, int k, float *out,
                             void *stream);
 
+// ---- verification (verify.hip) --------------------------------------------------------
+// counts[2j] += #{p : dist2(q_j, p) < thr[2j]}, counts[2j+1] += #{p : dist2(q_j, p) < thr[2j+1]}
+// over the n points (nq <= 1024 queries; counts zeroed by the caller, accumulated).
+int lsk_hip_count_below(const float *pts, int64_t n, const float *q, const float *thr, int nq,
+                        unsigned long long *counts, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

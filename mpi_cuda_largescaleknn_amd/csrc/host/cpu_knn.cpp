@@ -173,6 +173,25 @@ extern "C" void lsk_cpu_kth_brute(const float *pts, int64_t n, const float *qry,
   });
 }
 
+extern "C" void lsk_cpu_count_below(const float *pts, int64_t n, const float *qry,
+                                    const float *thr, int nq, unsigned long long *counts,
+                                    int nthreads) {
+  const vec3f *P = (const vec3f *)pts;
+  const vec3f *Q = (const vec3f *)qry;
+  parallel_for(nq, nthreads, [&](int64_t b, int64_t e) {
+    for (int64_t j = b; j < e; j++) {
+      unsigned long long lt = 0, le = 0;
+      for (int64_t i = 0; i < n; i++) {
+        const float v = lsk::dist2(Q[j], P[i]);
+        lt += v < thr[2 * j];
+        le += v < thr[2 * j + 1];
+      }
+      counts[2 * j] += lt;
+      counts[2 * j + 1] += le;
+    }
+  });
+}
+
 extern "C" void lsk_cpu_kth_kdtree(const float *pts, int64_t n, const float *qry, int64_t nq,
                                    int k, float cut2, float *out_d2, int nthreads) {
   KdTree t;

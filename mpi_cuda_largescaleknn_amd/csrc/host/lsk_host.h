@@ -73,6 +73,10 @@ float lsk_box_distance(const float *a, const float *b);
 // distance. cut2 = r*r (float) or +inf.
 void lsk_cpu_kth_brute(const float *pts, int64_t n, const float *qry, int64_t nq, int k,
                        float cut2, float *out_d2, int nthreads);
+// Verification counts (= lsk_hip_count_below): counts[2j] += #{p : dist2(q_j,p) < thr[2j]},
+// counts[2j+1] += #{p : dist2(q_j,p) < thr[2j+1]}.
+void lsk_cpu_count_below(const float *pts, int64_t n, const float *qry, const float *thr, int nq,
+                         unsigned long long *counts, int nthreads);
 // Same result via a CPU k-d tree (object-median, leaf buckets) built over `pts`.
 void lsk_cpu_kth_kdtree(const float *pts, int64_t n, const float *qry, int64_t nq, int k,
                         float cut2, float *out_d2, int nthreads);

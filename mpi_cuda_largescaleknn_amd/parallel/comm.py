@@ -20,6 +20,8 @@ Implementations:
 """
 from __future__ import annotations
 
+import math
+import os
 import threading
 from typing import Sequence
 
@@ -30,6 +32,14 @@ import torch.distributed as dist
 class Comm:
     rank: int = 0
     size: int = 1
+    # True: run every collective through the backend even on a 1-rank group, and the
+    # pipelines take their multi-rank path (tests: exercises each RCCL call site on one GPU)
+    force: bool = False
+
+    @property
+    def distributed(self) -> bool:
+        """Multi-rank code path: more than one rank, or a forced 1-rank group."""
+        return self.size > 1 or self.force
 
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         raise NotImplementedError
@@ -96,6 +106,14 @@ class SingleComm(Comm):
 
 _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
 
+# Largest single point-to-point message handed to the backend. RCCL 2.26 (torch 2.10's
+# librccl) corrupts the second half of any send/recv above 1 GiB (measured on MI355X with
+# a 1-rank group: 1024 MiB exact, 1025 MiB wrong from byte 2^29 on; all_to_all_single and
+# batch_isend_irecv alike; profiles/r2_rccl/README.txt). At 1B points on 2 ranks the
+# redistribution sends ~3 GB to the peer, so every larger message is split into rounds of
+# at most this many bytes per peer.
+MAX_MSG_BYTES = int(os.environ.get("LSKNN_MAX_MSG_MB", "256")) << 20
+
 
 class TorchComm(Comm):
     """torch.distributed process group (RCCL for GPU tensors, gloo for CPU).
@@ -104,20 +122,22 @@ class TorchComm(Comm):
     two ranks on one device) stages every collective through host memory, so the whole
     multi-process GPU pipeline can run on a one-GPU box (tests/test_gpu_multiprocess.py)."""
 
-    def __init__(self, device: torch.device | str, group=None):
+    def __init__(self, device: torch.device | str, group=None, force: bool = False):
         self.group = group
+        self.force = bool(force)
         self.rank = dist.get_rank(group)
         self.size = dist.get_world_size(group)
         self._device = torch.device(device)
         self.backend = dist.get_backend(group)
         self.staged = self.backend == "gloo" and self._device.type != "cpu"
+        self.max_msg_bytes = MAX_MSG_BYTES
 
     @property
     def device(self) -> torch.device:
         return self._device
 
     def allreduce_(self, t, op="sum"):
-        if self.size > 1:
+        if self.distributed:
             if self.staged and t.device.type != "cpu":
                 h = t.cpu()
                 dist.all_reduce(h, op=_OPS[op], group=self.group)
@@ -128,9 +148,9 @@ class TorchComm(Comm):
 
     def allgather(self, t):
         t = t.contiguous()
-        if self.staged and t.device.type != "cpu" and self.size > 1:
+        if self.staged and t.device.type != "cpu" and self.distributed:
             return self._gather_gloo(t.cpu()).to(t.device)
-        if self.size == 1:
+        if not self.distributed:
             out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
             out[0].copy_(t)
             return out
@@ -149,35 +169,69 @@ class TorchComm(Comm):
         send_counts = [int(c) for c in send_counts]
         recv_counts = self.exchange_counts(send_counts)
         row_shape = tuple(send.shape[1:])
-        if self.size == 1:
+        if not self.distributed:
             return send.clone(), recv_counts
         dev = send.device
         staged = self.staged and dev.type != "cpu"
         src = send.cpu() if staged else send.contiguous()
         recv = torch.empty((sum(recv_counts), *row_shape), dtype=send.dtype, device=src.device)
-        dist.all_to_all_single(recv, src, output_split_sizes=recv_counts,
-                               input_split_sizes=send_counts, group=self.group)
+        row_bytes = src.element_size() * math.prod(row_shape)
+        if max(send_counts + recv_counts + [0]) * row_bytes <= self.max_msg_bytes:
+            dist.all_to_all_single(recv, src, output_split_sizes=recv_counts,
+                                   input_split_sizes=send_counts, group=self.group)
+        else:
+            so, ro = _offsets(send_counts), _offsets(recv_counts)
+            sends = [(j, src[so[j]:so[j + 1]]) for j in range(self.size)]
+            recvs = [(j, recv[ro[j]:ro[j + 1]]) for j in range(self.size)]
+            self._p2p_rounds(sends, recvs)
         return (recv.to(dev) if staged else recv), recv_counts
+
+    def _p2p_rounds(self, sends, recvs):
+        """Grouped send/recv of contiguous tensors, every message cut into pieces of at
+        most max_msg_bytes: round r carries piece r of every pair (both ends know each
+        message's size, so the pieces match pair by pair in posting order). Own-rank
+        pairs are a local copy unless the group is forced (then RCCL carries them too)."""
+        cap = max(1, self.max_msg_bytes)
+        via_backend = self.force and self.backend == "nccl"  # own-rank pairs through RCCL
+
+        def pieces(t):
+            b = t.reshape(-1).view(torch.uint8)
+            return [b[o:o + cap] for o in range(0, b.numel(), cap)]
+
+        own = {}
+        ps, pr = [], []
+        for j, t in sends:
+            if j == self.rank and not via_backend:
+                own[j] = t
+            elif t.numel():
+                ps.append((j, pieces(t)))
+        for j, t in recvs:
+            if j == self.rank and not via_backend:
+                if t.numel():
+                    t.copy_(own[j])
+            elif t.numel():
+                pr.append((j, pieces(t)))
+        rounds = max([len(p) for _, p in ps + pr] + [0])
+        for r in range(rounds):
+            ops = [dist.P2POp(dist.isend, p[r], j, group=self.group) for j, p in ps if r < len(p)]
+            ops += [dist.P2POp(dist.irecv, p[r], j, group=self.group) for j, p in pr if r < len(p)]
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
 
     def p2p(self, sends, recvs):
         staged = self.staged
         bufdev = torch.device("cpu") if staged else self._device
         out = [torch.empty(shape, dtype=dt, device=bufdev) for _, shape, dt in recvs]
-        ops = [dist.P2POp(dist.isend, (t.cpu() if staged else t.contiguous()), dst, group=self.group)
-               for dst, t in sends if dst != self.rank]
-        ops += [dist.P2POp(dist.irecv, buf, src, group=self.group)
-                for (src, _, _), buf in zip(recvs, out) if src != self.rank]
-        own = {dst: t for dst, t in sends if dst == self.rank}
-        for (src, _, _), buf in zip(recvs, out):
-            if src == self.rank:
-                buf.copy_(own[src])
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        # own-rank traffic is a local copy, except on a forced group where it goes through
+        # the backend as well (RCCL send/recv to self inside the group); messages above
+        # max_msg_bytes travel in pieces (_p2p_rounds)
+        self._p2p_rounds([(dst, (t.cpu() if staged else t.contiguous())) for dst, t in sends],
+                         list(zip([src for src, _, _ in recvs], out)))
         return [b.to(self._device) for b in out] if staged else out
 
     def barrier(self):
-        if self.size > 1:
+        if self.distributed:
             if self.backend == "nccl":
                 # device barrier via a 1-element all-reduce keeps RCCL the only channel
                 t = torch.zeros(1, device=self._device)
@@ -187,6 +241,13 @@ class TorchComm(Comm):
                 if self._device.type == "cuda":
                     torch.cuda.synchronize(self._device)
                 dist.barrier(group=self.group)
+
+
+def _offsets(counts):
+    o = [0]
+    for c in counts:
+        o.append(o[-1] + int(c))
+    return o
 
 
 class _Hub:

@@ -84,6 +84,7 @@ class MonitoredComm(Comm):
         self.inner = inner
         self.rank = inner.rank
         self.size = inner.size
+        self.force = inner.force
         self.fault = fault if fault and fault["rank"] == inner.rank else None
         self.calls: dict[str, int] = {}
 

@@ -52,7 +52,13 @@ def _env_int(*names, default=None):
     return default
 
 
-def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False) -> Launch:
+def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False,
+         force_distributed: bool | None = None) -> Launch:
+    """Bootstrap this rank. `force_distributed` (default: env LSKNN_FORCE_DIST=1) builds a
+    process group and the multi-rank pipeline even for a single rank, so that a 1-GPU run
+    executes every collective through RCCL."""
+    if force_distributed is None:
+        force_distributed = os.environ.get("LSKNN_FORCE_DIST", "0") == "1"
     rank = _env_int("RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "PMIX_RANK", default=0)
     size = _env_int("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
     local = _env_int("LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", default=rank)
@@ -74,7 +80,7 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         device = torch.device("cpu")
     fault = F.parse_fault(os.environ.get("LSKNN_FAULT"))
     store = watchdog = None
-    if size > 1:
+    if size > 1 or force_distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(size)
@@ -90,7 +96,7 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
             dist.init_process_group("nccl", rank=rank, world_size=size, device_id=device, timeout=timeout)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
-        comm: Comm = TorchComm(device)
+        comm: Comm = TorchComm(device, force=force_distributed)
         store = dist.distributed_c10d._get_default_store()
         watchdog = F.Watchdog(rank, size, store).start()
     else:
@@ -102,7 +108,7 @@ def finalize(launch: Launch) -> None:
     # the watchdog stops first: peers leaving the final barrier early close the store
     if launch.watchdog is not None:
         launch.watchdog.stop()
-    if launch.size > 1 and dist.is_initialized():
+    if dist.is_initialized():
         launch.comm.barrier()
         dist.destroy_process_group()
 

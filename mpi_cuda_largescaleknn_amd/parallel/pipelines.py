@@ -75,7 +75,7 @@ class RunInfo:
 # --------------------------------------------------------------------------- helpers
 def global_box(points: torch.Tensor, comm: Comm) -> torch.Tensor:
     box = K.bounds(points)
-    if comm.size > 1:
+    if comm.distributed:
         v = torch.cat([box[0:3], -box[3:6]])
         comm.allreduce_(v, "min")
         box = torch.cat([v[0:3], -v[3:6], box[6:8]])
@@ -320,7 +320,8 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     box = global_box(points, comm)
     hint2 = E.radius_hint(box, n_total, cfg.k)
     info.timer.mark("bounds")
-    if comm.size == 1:
+    if not comm.distributed:
+        info.counts["owned_points"] = n_local
         index = E.build_index(points, box)
         info.timer.mark("build")
         # one rank: the k-NN kernel writes the final distances in input order (fused scatter)
@@ -357,19 +358,20 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     info.timer.start()
     points = points.contiguous()
     n_local = points.shape[0]
-    if comm.size == 1:
+    if not comm.distributed:
         n_total = n_local
     else:
         t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
         comm.allreduce_(t, "sum")
         n_total = int(t.item())
     box = K.bounds(points)
-    gbox = global_box(points, comm) if comm.size > 1 else box
+    gbox = global_box(points, comm) if comm.distributed else box
     hint2 = E.radius_hint(gbox, n_total, cfg.k)
     info.timer.mark("bounds")
     index = E.build_index(points, box)
+    info.counts["owned_points"] = n_local
     info.timer.mark("build")
-    if comm.size == 1:  # fused scatter: final distances straight from the k-NN kernel
+    if not comm.distributed:  # fused scatter: final distances straight from the k-NN kernel
         out = _check_out(out, n_local, points)
         E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
         info.timer.mark("knn_local")

@@ -39,6 +39,9 @@ def test_bench_single_rank_cpu():
     assert rec["n_gpus"] == 1 and rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True
     assert rec["config"]["all_finite"] is True
+    assert rec["config"]["sampled_exact"] == "256/256"
+    assert "(k=8) on 0.02M float3" in rec["metric"]
+    assert rec["detail"]["phase_ms_max_over_ranks"]["knn_local"] > 0
 
 
 @pytest.mark.gpu
@@ -53,6 +56,22 @@ def test_bench_single_gpu_graph_and_eager(graph):
     assert rec["n_gpus"] == 1 and rec["value"] > 0
     assert rec["config"]["all_finite"] is True
     assert rec["config"]["hip_graph"] is (graph == "1")
+    assert rec["config"]["sampled_exact"] == "256/256"
+
+
+@pytest.mark.gpu
+def test_bench_forced_rccl_single_gpu():
+    """One rank through the multi-rank pipeline on a real 1-rank RCCL group: every
+    collective of the step (all-reduce, all-gather, all-to-all-v) runs on RCCL."""
+    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
+                          "--force-dist"], cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1",
+                                                               MASTER_PORT=str(_free_port())),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["config"]["hip_graph"] is False
+    assert rec["config"]["sampled_exact"] == "256/256"
+    assert "alltoallv_points" in rec["detail"]["phase_ms_max_over_ranks"]
 
 
 @pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])
@@ -68,3 +87,20 @@ def test_bench_two_ranks_torchrun_gloo(variant):
     assert rec["config"]["global_batch"] == 30000
     assert rec["config"]["all_finite"] is True
     assert rec["ms_per_step"] > 0
+    d = rec["detail"]
+    assert len(d["knn_local_ms_per_rank"]) == 2
+    assert sum(d["owned_points_per_rank"]) == 30000
+    if variant == "unordered":
+        assert rec["config"]["sampled_exact"] == "256/256"
+        assert d["redistributed_bytes"] > 0
+
+
+def test_bench_global_set_independent_of_rank_count():
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    cpu = torch.device("cpu")
+    bench.GEN_CHUNK = 7000  # several chunk boundaries inside every block
+    one = bench.make_points(50000, 0, 1, cpu, "unordered")
+    parts = [bench.make_points(50000, r, 3, cpu, "unordered") for r in range(3)]
+    assert torch.equal(torch.cat(parts), one)

@@ -1,0 +1,91 @@
+"""Forced multi-rank path on a 1-rank gloo group (CPU): every pipeline goes through its
+collectives (TorchComm(force=True)) and equals the single-rank result bit for bit. The
+GPU twin on a real 1-rank RCCL group is tests/test_gpu_rccl.py."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+from datasets import clustered
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, out_dir):
+    import torch.distributed as dist
+
+    from mpi_cuda_largescaleknn_amd.models import knn_engine as E
+    from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL
+    from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA
+    from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    comm = TorchComm("cpu", force=True)
+    p = clustered(6000, seed=2)
+    cfg = E.KnnConfig(k=12)
+    res = {}
+    for name, fn in (("unordered", PL.unordered_knn), ("prepartitioned", PL.prepartitioned_knn),
+                     ("ring", RA.ring_knn), ("peer", RA.peer_knn)):
+        info = PL.RunInfo(PL.PhaseTimer(True, torch.device("cpu")))
+        res[name] = fn(p, comm, cfg, info)
+        res[name + "_single"] = fn(p, SingleComm("cpu"), cfg)
+        res[name + "_phases"] = sorted(info.timer.times)
+    torch.save(res, os.path.join(out_dir, "res.pt"))
+    dist.destroy_process_group()
+
+
+def test_forced_one_rank_gloo_equals_single(tmp_path):
+    mp.spawn(_worker, args=(_port(), str(tmp_path)), nprocs=1, join=True)
+    res = torch.load(tmp_path / "res.pt", weights_only=True)
+    for name in ("unordered", "prepartitioned", "ring", "peer"):
+        assert torch.equal(res[name], res[name + "_single"]), name
+    assert "alltoallv_points" in res["unordered_phases"]
+    assert "halo_alltoallv" in res["prepartitioned_phases"]
+
+
+def _chunk_worker(rank, size, port, out_dir):
+    import torch.distributed as dist
+
+    from mpi_cuda_largescaleknn_amd.parallel.comm import TorchComm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    comm = TorchComm("cpu")
+    comm.max_msg_bytes = 100  # force many rounds of pieces (uneven last pieces)
+    g = torch.Generator().manual_seed(rank)
+    counts = [(rank * 7 + 3 * j) % 11 + (40 if j == (rank + 1) % size else 0) for j in range(size)]
+    send = torch.rand((sum(counts), 3), generator=g)
+    recv, rc = comm.alltoallv(send, counts)
+    # ring p2p of a payload much larger than one piece
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+    big = torch.arange(1000, dtype=torch.float32) + 1000 * rank
+    (got,) = comm.p2p([(nxt, big)], [(prv, (1000,), torch.float32)])
+    torch.save({"send": send, "counts": counts, "recv": recv, "rc": rc, "got": got},
+               os.path.join(out_dir, f"{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_alltoallv_and_p2p_in_pieces_gloo(tmp_path):
+    size = 3
+    mp.spawn(_chunk_worker, args=(size, _port(), str(tmp_path)), nprocs=size, join=True)
+    r = [torch.load(tmp_path / f"{i}.pt", weights_only=True) for i in range(size)]
+    for me in range(size):
+        parts = []
+        for src in range(size):
+            c = r[src]["counts"]
+            o = sum(c[:me])
+            parts.append(r[src]["send"][o:o + c[me]])
+        assert torch.equal(r[me]["recv"], torch.cat(parts))
+        assert r[me]["rc"] == [r[src]["counts"][me] for src in range(size)]
+        prv = (me - 1) % size
+        assert torch.equal(r[me]["got"], torch.arange(1000, dtype=torch.float32) + 1000 * prv)

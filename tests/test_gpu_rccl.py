@@ -1,0 +1,101 @@
+"""RCCL call sites on one MI355X: a real 1-rank ``nccl`` (RCCL) process group with
+``TorchComm(force=True)`` runs every collective through RCCL and every pipeline through
+its multi-rank path (spatial redistribution all-to-all-v, halo all-gather/all-to-all-v,
+result return, ring/peer point-to-point). Outputs must equal the single-rank path bit
+for bit. RCCL refuses two ranks on one GPU, so this (plus the gloo multi-process tests)
+is what one GPU can show of the 8-GPU path."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from datasets import clustered
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, out_dir):
+    import torch.distributed as dist
+
+    from mpi_cuda_largescaleknn_amd.models import knn_engine as E
+    from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL
+    from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA
+    from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm, TorchComm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    comm = TorchComm(dev, force=True)
+    assert comm.backend == "nccl" and comm.distributed and not comm.staged
+    one = SingleComm(dev)
+    p = clustered(60000, seed=11).to(dev)
+    cfg = E.KnnConfig(k=24)
+    res = {}
+    # raw collectives on RCCL
+    t = torch.arange(6, dtype=torch.float32, device=dev)
+    comm.allreduce_(t, "max")
+    res["allgather"] = comm.allgather(t).cpu()
+    rows = torch.arange(30, dtype=torch.float32, device=dev).view(10, 3)
+    res["alltoallv"], _ = comm.alltoallv(rows, [10])
+    res["alltoallv"] = res["alltoallv"].cpu()
+    (res["p2p"],) = comm.p2p([(0, rows)], [(0, (10, 3), torch.float32)])
+    res["p2p"] = res["p2p"].cpu()
+    comm.barrier()
+    for name, fn in (("unordered", PL.unordered_knn), ("prepartitioned", PL.prepartitioned_knn),
+                     ("ring", RA.ring_knn), ("peer", RA.peer_knn)):
+        info = PL.RunInfo(PL.PhaseTimer(False, dev))
+        res[name] = fn(p, comm, cfg, info).cpu()
+        res[name + "_single"] = fn(p, one, cfg).cpu()
+        res[name + "_counts"] = dict(info.counts)
+    # messages above RCCL's 1 GiB limit (comm.MAX_MSG_BYTES) travel in pieces
+    big = torch.arange(400_000_000, dtype=torch.int32, device=dev).view(-1, 4)  # 1.6 GB
+    got, _ = comm.alltoallv(big, [big.shape[0]])
+    res["big_alltoallv_equal"] = bool(torch.equal(got, big))
+    del got
+    (got,) = comm.p2p([(0, big)], [(0, tuple(big.shape), torch.int32)])
+    res["big_p2p_equal"] = bool(torch.equal(got, big))
+    torch.save(res, os.path.join(out_dir, "res.pt"))
+    dist.destroy_process_group()
+
+
+def test_forced_one_rank_rccl_pipelines_equal_single_rank(tmp_path):
+    mp.spawn(_worker, args=(_port(), str(tmp_path)), nprocs=1, join=True)
+    res = torch.load(tmp_path / "res.pt", weights_only=True)
+    rows = torch.arange(30, dtype=torch.float32).view(10, 3)
+    assert torch.equal(res["allgather"], torch.arange(6, dtype=torch.float32)[None])
+    assert torch.equal(res["alltoallv"], rows) and torch.equal(res["p2p"], rows)
+    assert res["big_alltoallv_equal"] and res["big_p2p_equal"]
+    for name in ("unordered", "prepartitioned", "ring", "peer"):
+        assert torch.equal(res[name], res[name + "_single"]), name
+        assert torch.isfinite(res[name]).all()
+    # the unordered run went through the redistribution (all 60000 points owned)
+    assert res["unordered_counts"]["owned_points"] == 60000
+
+
+def test_count_below_gpu_equals_cpu():
+    from mpi_cuda_largescaleknn_amd.utils import verify as V
+
+    g = torch.Generator().manual_seed(4)
+    pts = torch.rand((300_001, 3), generator=g)
+    q = torch.rand((700, 3), generator=g)
+    thr = torch.rand((700, 2), generator=g) * 0.05
+    cpu = torch.zeros((700, 2), dtype=torch.int64)
+    V.count_below(pts, q, thr, cpu)
+    gpu = torch.zeros((700, 2), dtype=torch.int64, device="cuda")
+    V.count_below(pts, q.cuda(), thr.cuda(), gpu, chunk=100_000)  # host chunks streamed
+    assert torch.equal(gpu.cpu(), cpu)
+    gpu.zero_()
+    V.count_below(pts.cuda(), q.cuda(), thr.cuda(), gpu)
+    assert torch.equal(gpu.cpu(), cpu)
