@@ -178,6 +178,8 @@ def main():
                 _step()
         torch.cuda.current_stream(device).wait_stream(side)
         _sync(device)
+        # over-full key cells seen by the eager warmup: capture the (fixed-size) refinement
+        E.REFINE_CAPTURE = E.LAST_REFINED
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             _step()
@@ -204,8 +206,10 @@ def main():
 
     ms = elapsed / args.steps * 1e3
     value = n_total * args.steps / elapsed / 1e6
+    heavy_unrefined = False
     if graph is not None:
         E.verify_captured_failures(clear=True)  # raises if a replay overflowed a failure list
+        heavy_unrefined = E.captured_heavy_cells(clear=True)
     finite_t = torch.tensor([0 if host_out.numel() == 0 or bool(torch.isfinite(host_out).all()) else 1],
                             dtype=torch.int64, device=device)
     comm.allreduce_(finite_t, "sum")
@@ -243,6 +247,7 @@ def main():
                                 else f"halo x{world}"),
                 "k": args.k,
                 "hip_graph": graph is not None,
+                "heavy_cells_unrefined": heavy_unrefined,
                 "all_finite": finite,
                 "sampled_exact": (f"{check['exact']}/{check['samples']}" if check else None),
             },

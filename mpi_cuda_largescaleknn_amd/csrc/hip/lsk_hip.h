@@ -57,6 +57,12 @@ int lsk_hip_key_histogram(const uint32_t *keys, int64_t n, int shift, int sample
 int lsk_hip_count_dest(const uint32_t *dest, int64_t n, int ndest, uint32_t *counts,
                        void *stream);
 
+// Bounding boxes of contiguous segments: seg[i] (non-decreasing runs) = segment of point
+// i; lo/hi: [nseg][3] floats (overwritten). Wave reductions + one atomic per segment and
+// wave (no contended per-point atomics).
+int lsk_hip_segment_bounds(const float *pts, const uint32_t *seg, int64_t m, int64_t nseg,
+                           float *lo, float *hi, void *stream);
+
 // ---- LSD radix sort of (uint32 key, uint32 value) pairs ------------------------------
 size_t lsk_hip_sort_ws_bytes(int64_t n);
 // Sorts by key bits [0, key_bits). Uses keys_alt/vals_alt as ping-pong buffers;

@@ -310,3 +310,112 @@ extern "C" int lsk_hip_count_dest(const uint32_t *dest, int64_t n, int ndest, ui
   LSK_CHECK_LAUNCH("count_dest");
   return 0;
 }
+
+// ---- per-segment bounding boxes (heavy-cell refinement, knn_engine.refine_heavy_cells)
+namespace {
+
+// order-preserving float <-> uint map (atomicMin/Max on uint = float min/max)
+__device__ __forceinline__ uint32_t ord_of(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+constexpr int kSegPer = 16;  // elements per lane
+
+// Segments are contiguous runs of equal seg ids. A wave takes 64 x kSegPer consecutive
+// elements; lanes reduce their own elements while the id stays the same, then a wave
+// reduction per distinct id (wave-uniform loop over the few ids in the window) and one
+// atomic per (wave, id, component): a 1e7-point segment costs ~1e4 atomics per address,
+// not 1e7 contended compare-and-swaps (torch.scatter_reduce).
+__global__ __launch_bounds__(256) void segment_bounds_kernel(const float *__restrict__ p,
+                                                             const uint32_t *__restrict__ seg,
+                                                             int64_t m, uint32_t *__restrict__ lo,
+                                                             uint32_t *__restrict__ hi) {
+  const int lane = lsk::lane_id();
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = (((int64_t)blockIdx.x * blockDim.x) >> 6) + (threadIdx.x >> 6);
+       w * 64 * kSegPer < m; w += nwaves) {
+    const int64_t base = w * 64 * kSegPer;
+    const int64_t end = base + 64 * kSegPer < m ? base + 64 * kSegPer : m;
+    // lane l handles elements base + l*kSegPer ... (contiguous per lane)
+    const int64_t b0 = base + (int64_t)lane * kSegPer;
+    uint32_t cur = 0xffffffffu;
+    uint32_t l0 = 0xffffffffu, l1 = 0xffffffffu, l2 = 0xffffffffu, h0 = 0, h1 = 0, h2 = 0;
+    auto flush = [&]() {
+      if (cur != 0xffffffffu) {
+        atomicMin(&lo[3 * (int64_t)cur], l0); atomicMin(&lo[3 * (int64_t)cur + 1], l1);
+        atomicMin(&lo[3 * (int64_t)cur + 2], l2);
+        atomicMax(&hi[3 * (int64_t)cur], h0); atomicMax(&hi[3 * (int64_t)cur + 1], h1);
+        atomicMax(&hi[3 * (int64_t)cur + 2], h2);
+      }
+    };
+    // fast path: the whole window is one segment -> one wave reduction, lane 0 flushes
+    const uint32_t s_first = seg[base], s_last = seg[end - 1];
+    if (s_first == s_last) {
+      for (int j = 0; j < kSegPer; j++) {
+        const int64_t i = b0 + j;
+        if (i < end) {
+          const uint32_t x = ord_of(p[3 * i]), y = ord_of(p[3 * i + 1]), z = ord_of(p[3 * i + 2]);
+          l0 = min(l0, x); l1 = min(l1, y); l2 = min(l2, z);
+          h0 = max(h0, x); h1 = max(h1, y); h2 = max(h2, z);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        l0 = min(l0, (uint32_t)__shfl_xor((int)l0, o)); l1 = min(l1, (uint32_t)__shfl_xor((int)l1, o));
+        l2 = min(l2, (uint32_t)__shfl_xor((int)l2, o)); h0 = max(h0, (uint32_t)__shfl_xor((int)h0, o));
+        h1 = max(h1, (uint32_t)__shfl_xor((int)h1, o)); h2 = max(h2, (uint32_t)__shfl_xor((int)h2, o));
+      }
+      if (lane == 0) {
+        cur = s_first;
+        flush();
+      }
+      continue;
+    }
+    // boundary window: per-lane runs, one flush per lane-run
+    for (int j = 0; j < kSegPer; j++) {
+      const int64_t i = b0 + j;
+      if (i >= end) break;
+      const uint32_t s = seg[i];
+      if (s != cur) {
+        flush();
+        cur = s;
+        l0 = l1 = l2 = 0xffffffffu;
+        h0 = h1 = h2 = 0u;
+      }
+      const uint32_t x = ord_of(p[3 * i]), y = ord_of(p[3 * i + 1]), z = ord_of(p[3 * i + 2]);
+      l0 = min(l0, x); l1 = min(l1, y); l2 = min(l2, z);
+      h0 = max(h0, x); h1 = max(h1, y); h2 = max(h2, z);
+    }
+    flush();
+  }
+}
+
+__global__ __launch_bounds__(256) void ord_to_float_kernel(uint32_t *__restrict__ v, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t u = v[i];
+    v[i] = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  }
+}
+
+}  // namespace
+
+extern "C" int lsk_hip_segment_bounds(const float *pts, const uint32_t *seg, int64_t m, int64_t nseg,
+                                      float *lo, float *hi, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (nseg <= 0) return 0;
+  LSK_HIP(hipMemsetAsync(lo, 0xff, (size_t)nseg * 3 * sizeof(float), s));
+  LSK_HIP(hipMemsetAsync(hi, 0x00, (size_t)nseg * 3 * sizeof(float), s));
+  if (m > 0) {
+    segment_bounds_kernel<<<lsk_blocks(m, 256 * kSegPer, 8192), 256, 0, s>>>(
+        pts, seg, m, (uint32_t *)lo, (uint32_t *)hi);
+    LSK_CHECK_LAUNCH("segment_bounds");
+  }
+  const int64_t tot = nseg * 3;
+  ord_to_float_kernel<<<lsk_blocks(tot, 256 * 4, 8192), 256, 0, s>>>((uint32_t *)lo, tot);
+  LSK_CHECK_LAUNCH("segment_bounds_lo");
+  ord_to_float_kernel<<<lsk_blocks(tot, 256 * 4, 8192), 256, 0, s>>>((uint32_t *)hi, tot);
+  LSK_CHECK_LAUNCH("segment_bounds_hi");
+  return 0;
+}

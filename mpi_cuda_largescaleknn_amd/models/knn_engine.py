@@ -103,6 +103,14 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None) -> LocalI
 
 
 HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key
+# HIP-graph captures cannot ask the host whether a cell is over-full. REFINE_CAPTURE
+# (set by the caller from an eager warmup on the same kind of data, see LAST_REFINED)
+# captures the refinement with fixed, data-independent sizes; otherwise the capture
+# records a device flag (CAPTURED_HEAVY) that says after a replay whether some cell
+# would have needed it (results stay exact either way, only the speed differs).
+REFINE_CAPTURE = False
+LAST_REFINED = False
+CAPTURED_HEAVY: list = []
 
 
 def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
@@ -110,42 +118,103 @@ def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Te
 
     Keys have 10 bits per axis of the global cube, so a cluster much smaller than one
     cell (huge dynamic range, e.g. a dense core in a large box) shares a single key and
-    its buckets all overlap: the k-NN walk cannot cull inside it. When some cell holds
-    more than HEAVY_RUN sorted points, every cell's points are re-keyed on the curve of
-    the cell's own bounding box and the order becomes (cell, local key) — two more
-    stable passes of the same radix sort. Only the order changes (results are exact in
-    any order). Skipped while a HIP graph is being captured (the check needs the host);
-    one compare pass + one host sync otherwise."""
+    its buckets all overlap: the k-NN walk cannot cull inside it. The points of every
+    run of more than HEAVY_RUN equal keys are re-keyed on the curve of the run's own
+    bounding box and re-sorted by (run, local key) with the same radix sort; only the
+    order changes (results are exact in any order). Eager: one compare pass + one host
+    sync, then work and memory proportional to the over-full runs only. Inside a HIP
+    graph capture: see REFINE_CAPTURE."""
+    global LAST_REFINED
     n = skeys.shape[0]
     if n <= HEAVY_RUN:
         return perm
-    gpu = K.is_gpu(skeys)
-    if gpu and torch.cuda.is_current_stream_capturing():
+    heavy_any = (skeys[HEAVY_RUN:] == skeys[:-HEAVY_RUN]).any()
+    if K.is_gpu(skeys) and torch.cuda.is_current_stream_capturing():
+        if REFINE_CAPTURE:
+            return _refine_all_cells(points, skeys, perm)
+        CAPTURED_HEAVY.append(heavy_any)
         return perm
-    if not bool((skeys[HEAVY_RUN:] == skeys[:-HEAVY_RUN]).any()):
+    if not bool(heavy_any):
         return perm
+    LAST_REFINED = True
+    return _refine_heavy_runs(points, skeys, perm)
+
+
+def _local_keys(p: torch.Tensor, seg: torch.Tensor, nseg: int) -> torch.Tensor:
+    """30-bit curve keys of points p on the bounding box of their segment."""
+    dev = p.device
+    if K.is_gpu(p):
+        lo, hi = K.segment_bounds(p, seg, nseg)
+    else:
+        idx3 = seg.long()[:, None].expand(-1, 3)
+        lo = torch.full((nseg, 3), math.inf, device=dev).scatter_reduce(0, idx3, p, "amin")
+        hi = torch.full((nseg, 3), -math.inf, device=dev).scatter_reduce(0, idx3, p, "amax")
+    ext = hi - lo
+    ext = torch.where(ext > 0, ext, torch.ones_like(ext))
+    sl = seg.long()
+    q = ((p - lo[sl]) / ext[sl]).clamp_(0.0, 1.0).contiguous()
+    del sl
+    del lo, hi, ext
+    # unit cube, scale just under 1024 cells so q = 1 stays in the last cell
+    # (filled on the device: a host-to-device copy is not allowed inside a graph capture)
+    unit = torch.ones(8, dtype=torch.float32, device=dev)
+    unit[0:3].zero_()
+    unit[6:7].fill_(1023.5)
+    k2, _ = K.morton(q, unit, with_iota=False)
+    return k2
+
+
+def _refine_heavy_runs(points, skeys, perm):
+    """Eager refinement restricted to the over-full runs (m points): O(m) memory."""
+    n = skeys.shape[0]
     dev = skeys.device
     brk = torch.ones(n, dtype=torch.bool, device=dev)
     brk[1:] = skeys[1:] != skeys[:-1]
-    rid = torch.cumsum(brk, 0, dtype=torch.int64) - 1
-    nr = int(rid[-1]) + 1
-    p = points[perm.long()]
-    idx3 = rid[:, None].expand(-1, 3)
-    lo = torch.full((nr, 3), math.inf, device=dev).scatter_reduce(0, idx3, p, "amin")
-    hi = torch.full((nr, 3), -math.inf, device=dev).scatter_reduce(0, idx3, p, "amax")
-    ext = hi - lo
-    ext = torch.where(ext > 0, ext, torch.ones_like(ext))
-    q = ((p - lo[rid]) / ext[rid]).clamp_(0.0, 1.0).contiguous()
-    del p, lo, hi, ext
-    # unit cube, scale just under 1024 cells so q = 1 stays in the last cell
-    unit = torch.tensor([0.0, 0.0, 0.0, 1.0, 1.0, 1.0, 1023.5, 1.0], dtype=torch.float32, device=dev)
-    k2, _ = K.morton(q, unit, with_iota=False)
-    del q
+    starts = torch.nonzero(brk).view(-1)
+    ends = torch.cat([starts[1:], torch.tensor([n], dtype=starts.dtype, device=dev)])
+    lens = ends - starts
+    heavy = lens > HEAVY_RUN
+    hs, hl = starts[heavy], lens[heavy]
+    nh = int(hs.shape[0])
+    m = int(hl.sum())
+    seg = torch.repeat_interleave(torch.arange(nh, device=dev, dtype=torch.int32), hl)  # [m]
+    first = torch.cumsum(hl, 0) - hl                                          # run offsets in [m]
+    pos = hs[seg] + (torch.arange(m, device=dev) - first[seg])                # sorted positions
+    del brk, starts, ends, lens, heavy
+    src = perm[pos].long()
+    k2 = _local_keys(points[src], seg, nh)
+    loc = torch.arange(m, dtype=torch.int32, device=dev)
+    _, o1 = K.sort_pairs(k2, loc, 30)  # by local key ...
+    sbits = max(1, (nh - 1).bit_length())
+    _, o2 = K.sort_pairs(seg[o1.long()], o1, sbits)  # ... then stably by run
+    out = perm.clone()
+    out[pos] = perm[pos[o2.long()]]
+    return out
+
+
+def _refine_all_cells(points, skeys, perm):
+    """Graph-capturable refinement: every cell re-keyed, all sizes bounded by n (no host
+    sync; ~100 B per point of temporaries — used only when an eager warmup refined)."""
+    n = skeys.shape[0]
+    dev = skeys.device
+    brk = torch.ones(n, dtype=torch.bool, device=dev)
+    brk[1:] = skeys[1:] != skeys[:-1]
+    rid = (torch.cumsum(brk, 0, dtype=torch.int32) - 1).contiguous()
+    del brk
+    k2 = _local_keys(points[perm.long()], rid, n)
     pos = torch.arange(n, dtype=torch.int32, device=dev)
-    _, o1 = K.sort_pairs(k2, pos, 30)  # by local key ...
-    rbits = max(1, (nr - 1).bit_length())
-    _, o2 = K.sort_pairs(rid.to(torch.int32)[o1.long()], o1, rbits)  # ... then stably by cell
+    _, o1 = K.sort_pairs(k2, pos, 30)
+    rbits = max(1, (n - 1).bit_length())
+    _, o2 = K.sort_pairs(rid[o1.long()], o1, rbits)
     return perm[o2.long()].contiguous()
+
+
+def captured_heavy_cells(clear: bool = False) -> bool:
+    """After a replay: whether a captured build met an over-full cell it did not refine."""
+    hit = any(bool(f) for f in CAPTURED_HEAVY)
+    if clear:
+        CAPTURED_HEAVY.clear()
+    return hit
 
 
 def radius_hint2(box: torch.Tensor, n_total: int, k: int) -> float:

@@ -114,6 +114,16 @@ def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, key_bits: int = 30):
     return (ka, va) if alt.value else (keys, vals)
 
 
+def segment_bounds(p: torch.Tensor, seg: torch.Tensor, nseg: int):
+    """Per-segment AABB of GPU points p [m,3] with contiguous segment ids seg (int32,
+    non-decreasing runs) -> (lo, hi) [nseg, 3]."""
+    lo = torch.empty((nseg, 3), dtype=torch.float32, device=p.device)
+    hi = torch.empty((nseg, 3), dtype=torch.float32, device=p.device)
+    check(_native.hip().lsk_hip_segment_bounds(_ptr(p.contiguous()), _ptr(seg.contiguous()), p.shape[0], nseg,
+                                               _ptr(lo), _ptr(hi), _stream(p)), "segment_bounds")
+    return lo, hi
+
+
 def gather3(src: torch.Tensor, idx: torch.Tensor, pad: int = 0) -> torch.Tensor:
     """dst[i] = src[idx[i]] for float3 rows; dst gets `pad` extra zero rows."""
     n = idx.shape[0]

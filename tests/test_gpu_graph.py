@@ -54,3 +54,72 @@ def test_graph_replay_matches_eager_on_new_data(variant, k):
         torch.cuda.synchronize()
         ref = E.knn_distances(data.to(DEV), k).cpu()
         assert torch.equal(host_out, ref)
+
+
+def _capture(fn):
+    side = torch.cuda.Stream(DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        fn()
+    torch.cuda.current_stream(DEV).wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    torch.cuda.synchronize()
+    return g
+
+
+def test_graph_with_heavy_cell_refinement(monkeypatch):
+    """mixed_scale (a sub-cell core): the eager warmup refines, the capture then records
+    the fixed-size refinement; replay == eager bit for bit and about as fast."""
+    import time
+
+    from datasets import mixed_scale
+
+    n, k = 2_000_000, 100
+    data = mixed_scale(n, seed=4)
+    host_pts = torch.empty((n, 3), dtype=torch.float32, pin_memory=True)
+    host_pts.copy_(data)
+    out = torch.empty(n, dtype=torch.float32, device=DEV)
+
+    def body():
+        out.copy_(E.knn_distances(host_pts.to(DEV, non_blocking=True), k))
+
+    monkeypatch.setattr(E, "LAST_REFINED", False)
+    body()
+    torch.cuda.synchronize()
+    assert E.LAST_REFINED
+    t = time.perf_counter()
+    body()
+    torch.cuda.synchronize()
+    eager_s = time.perf_counter() - t
+    eager = out.cpu()
+    monkeypatch.setattr(E, "REFINE_CAPTURE", True)
+    g = _capture(body)
+    out.fill_(-1)
+    t = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    graph_s = time.perf_counter() - t
+    assert not E.captured_heavy_cells(clear=True)
+    E.verify_captured_failures(clear=True)
+    assert torch.equal(out.cpu(), eager)
+    print(f"mixed_scale 2e6 k=100: eager {eager_s * 1e3:.1f} ms, graph {graph_s * 1e3:.1f} ms")
+    assert graph_s < 1.5 * eager_s + 0.02
+
+
+def test_graph_without_refinement_flags_heavy_cells(monkeypatch):
+    from datasets import mixed_scale
+
+    n, k = 40_000, 16
+    data = mixed_scale(n, seed=6).to(DEV)
+    out = torch.empty(n, dtype=torch.float32, device=DEV)
+    monkeypatch.setattr(E, "REFINE_CAPTURE", False)
+    E.CAPTURED_HEAVY.clear()
+    g = _capture(lambda: out.copy_(E.knn_distances(data, k)))
+    g.replay()
+    torch.cuda.synchronize()
+    assert E.captured_heavy_cells(clear=True)
+    E.verify_captured_failures(clear=True)
+    assert torch.equal(out.cpu(), E.knn_distances(data, k).cpu())  # exact, only unrefined

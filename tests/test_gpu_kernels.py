@@ -329,3 +329,16 @@ def test_exact_kernel_large_k_and_cutoff():
         got = E.knn_distances(p.to(DEV), k, max_radius=r).cpu()
         ref = K.finalize_distances(K.kth_cpu(p, p[:300], k, E.cut2_of(r), "brute"))
         assert torch.equal(got[:300], ref), (k, r)
+
+
+def test_segment_bounds_kernel_matches_torch():
+    g = torch.Generator().manual_seed(9)
+    lens = torch.tensor([1, 5, 70000, 3, 1024 * 16, 64 * 16 + 1, 2, 300000], dtype=torch.int64)
+    m = int(lens.sum())
+    seg = torch.repeat_interleave(torch.arange(lens.shape[0], dtype=torch.int32), lens)
+    p = (torch.randn((m, 3), generator=g) * 100).float()
+    lo, hi = K.segment_bounds(p.cuda(), seg.cuda(), lens.shape[0])
+    idx3 = seg.long()[:, None].expand(-1, 3)
+    rlo = torch.full((lens.shape[0], 3), float("inf")).scatter_reduce(0, idx3, p, "amin")
+    rhi = torch.full((lens.shape[0], 3), -float("inf")).scatter_reduce(0, idx3, p, "amax")
+    assert torch.equal(lo.cpu(), rlo) and torch.equal(hi.cpu(), rhi)

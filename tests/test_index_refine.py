@@ -46,3 +46,20 @@ def test_uniform_data_is_not_reordered():
     keys, iota = K.morton(p, K.bounds(p))
     skeys, perm = K.sort_pairs(keys, iota, 30)
     assert E.refine_heavy_cells(p, skeys, perm) is perm
+
+
+def test_run_local_refinement_touches_only_heavy_runs():
+    p = mixed_scale(30000, seed=5)
+    keys, iota = K.morton(p, K.bounds(p))
+    skeys, perm = K.sort_pairs(keys, iota, 30)
+    a = E._refine_heavy_runs(p, skeys, perm)
+    b = E._refine_all_cells(p, skeys, perm)
+    brk = torch.ones(skeys.shape[0], dtype=torch.bool)
+    brk[1:] = skeys[1:] != skeys[:-1]
+    rid = torch.cumsum(brk.long(), 0) - 1
+    runlen = torch.bincount(rid)[rid]
+    heavy = runlen > E.HEAVY_RUN
+    assert heavy.sum() >= 15000
+    assert torch.equal(a[~heavy], perm[~heavy])      # light runs untouched
+    assert torch.equal(a[heavy], b[heavy])           # same order as the all-cells variant
+    assert torch.equal(torch.sort(a.long()).values, torch.arange(p.shape[0]))
