@@ -40,7 +40,10 @@ class CliArgs(C.Structure):
         ("device", C.c_char * 16),
         ("stats", C.c_char * 4096),
         ("verbose", C.c_int),
-        ("leaf_size", C.c_int),
+        ("bootstrap", C.c_char * 16),
+        ("nproc", C.c_int),
+        ("device_map", C.c_char * 256),
+        ("balance", C.c_char * 8),
     ]
 
 

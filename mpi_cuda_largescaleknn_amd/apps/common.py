@@ -68,6 +68,18 @@ def guarded(launch: Launch, fn) -> int:
         return 1
 
 
+def without_spawn(argv: list[str]) -> list[str]:
+    """argv minus `--bootstrap spawn` and `--nproc N` (the children's command line)."""
+    out, i = [], 0
+    while i < len(argv):
+        if argv[i] in ("--bootstrap", "--nproc") and i + 1 < len(argv):
+            i += 2
+            continue
+        out.append(argv[i])
+        i += 1
+    return out
+
+
 def fail(msg: str, code: int = 1) -> None:
     sys.stderr.write(msg + "\n")
     sys.exit(code)

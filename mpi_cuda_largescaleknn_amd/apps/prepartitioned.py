@@ -2,6 +2,8 @@
 
     hipKNN_prePartitionedData <fileList.txt> -o <prefix> -k <k> [-r <maxRadius>] [-g <gpusPerNode>]
                               [--mode auto|halo|peer] [--device auto|cuda|cpu] [--stats s.json] [-v]
+                              [--balance auto|on|off] [--bootstrap auto|env|mpi|spawn --nproc N]
+                              [--device-map 0,1,..]
 
 Same grammar and files as cudaMpiKNN_prePartitionedData
 (prePartitionedDataVariant.cu:176-389): line r of the list is rank r's float3 file,
@@ -34,7 +36,10 @@ def main(argv: list[str] | None = None) -> int:
     if args.mode == "ring":
         common.fail("Error: --mode ring applies to hipKNN_unorderedData")
     names = io.read_file_list(args.input)
-    launch = L.init(args.device, args.gpu_affinity, args.verbose)
+    if args.bootstrap == "spawn":
+        return L.spawn_local(args.nproc, "mpi_cuda_largescaleknn_amd.apps.prepartitioned", common.without_spawn(argv[1:]))
+    launch = L.init(args.device, args.gpu_affinity, args.verbose, bootstrap=args.bootstrap,
+                    device_map=args.device_map)
     return common.guarded(launch, lambda: _run(args, launch, names))
 
 
@@ -58,7 +63,7 @@ def _run(args, launch, names) -> int:
         host_out = (torch.empty(pts.shape[0], dtype=torch.float32, pin_memory=True)
                     if launch.device.type == "cuda" and not launch.comm.distributed
                     and PL.direct_host_out_pays(cfg.k) else None)
-        out = PL.prepartitioned_knn(dpts, launch.comm, cfg, info, out=host_out)
+        out = PL.prepartitioned_knn(dpts, launch.comm, cfg, info, out=host_out, balance=args.balance)
     res = out.cpu()
     if launch.device.type == "cuda":
         torch.cuda.synchronize(launch.device)

@@ -2,6 +2,7 @@
 
     hipKNN_unorderedData <in.float3> -o <out.float> -k <k> [-r <maxRadius>] [-g <gpusPerNode>]
                          [--mode auto|halo|ring] [--device auto|cuda|cpu] [--stats s.json] [-v]
+                         [--bootstrap auto|env|mpi|spawn --nproc N] [--device-map 0,1,..]
 
 Same grammar, input and output bytes as cudaMpiKNN_unorderedData
 (unorderedDataVariant.cu:105-239): rank r of P reads the block
@@ -29,7 +30,10 @@ def main(argv: list[str] | None = None) -> int:
     args = cli.parse_or_exit(cli.UNORDERED, argv)
     if args.mode == "peer":
         common.fail("Error: --mode peer applies to hipKNN_prePartitionedData")
-    launch = L.init(args.device, args.gpu_affinity, args.verbose)
+    if args.bootstrap == "spawn":
+        return L.spawn_local(args.nproc, "mpi_cuda_largescaleknn_amd.apps.unordered", common.without_spawn(argv[1:]))
+    launch = L.init(args.device, args.gpu_affinity, args.verbose, bootstrap=args.bootstrap,
+                    device_map=args.device_map)
     return common.guarded(launch, lambda: _run(args, launch))
 
 

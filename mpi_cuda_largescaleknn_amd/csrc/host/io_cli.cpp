@@ -28,7 +28,7 @@
 #include <thread>
 #include <vector>
 
-extern "C" int lsk_host_abi_version(void) { return 1; }
+extern "C" int lsk_host_abi_version(void) { return 2; }
 
 // ============================================================================ CLI
 namespace {
@@ -55,7 +55,8 @@ extern "C" int lsk_cli_parse(int variant, int argc, const char **argv, lsk_cli_a
   out->max_radius = std::numeric_limits<float>::infinity();
   copy_str(out->mode, sizeof(out->mode), "auto");
   copy_str(out->device, sizeof(out->device), "auto");
-  out->leaf_size = 64;
+  copy_str(out->bootstrap, sizeof(out->bootstrap), "auto");
+  copy_str(out->balance, sizeof(out->balance), "auto");
   std::string input, output;
 
   auto need_value = [&](int i, const std::string &flag) -> bool {
@@ -97,9 +98,31 @@ extern "C" int lsk_cli_parse(int variant, int argc, const char **argv, lsk_cli_a
     } else if (arg == "--stats") {
       if (!need_value(i, arg)) return 1;
       copy_str(out->stats, sizeof(out->stats), argv[++i]);
-    } else if (arg == "--leaf-size") {
+    } else if (arg == "--bootstrap") {
       if (!need_value(i, arg)) return 1;
-      out->leaf_size = std::atoi(argv[++i]);
+      std::string b = argv[++i];
+      if (b != "auto" && b != "env" && b != "mpi" && b != "spawn")
+        return usage_error("invalid --bootstrap '" + b + "' (auto|env|mpi|spawn)", err, errlen);
+      copy_str(out->bootstrap, sizeof(out->bootstrap), b);
+    } else if (arg == "--nproc") {
+      if (!need_value(i, arg)) return 1;
+      out->nproc = std::atoi(argv[++i]);
+      if (out->nproc < 1 || out->nproc > 1024)
+        return usage_error("invalid --nproc (1..1024)", err, errlen);
+    } else if (arg == "--device-map") {
+      if (!need_value(i, arg)) return 1;
+      std::string m = argv[++i];
+      bool ok = !m.empty() && m.size() < sizeof(out->device_map) && m.front() != ',' && m.back() != ',';
+      for (size_t c = 0; ok && c < m.size(); c++)
+        ok = (m[c] >= '0' && m[c] <= '9') || (m[c] == ',' && m[c - 1] != ',');
+      if (!ok) return usage_error("invalid --device-map '" + m + "' (e.g. 0,1,2,3)", err, errlen);
+      copy_str(out->device_map, sizeof(out->device_map), m);
+    } else if (arg == "--balance") {
+      if (!need_value(i, arg)) return 1;
+      std::string b = argv[++i];
+      if (b != "auto" && b != "on" && b != "off")
+        return usage_error("invalid --balance '" + b + "' (auto|on|off)", err, errlen);
+      copy_str(out->balance, sizeof(out->balance), b);
     } else if (arg == "-v" || arg == "--verbose") {
       out->verbose = 1;
     } else {
@@ -116,6 +139,8 @@ extern "C" int lsk_cli_parse(int variant, int argc, const char **argv, lsk_cli_a
                                     : "no output file(s) prefix specified",
                        err, errlen);
   if (out->k < 1) return usage_error("no k specified, or invalid k value", err, errlen);
+  if ((std::string(out->bootstrap) == "spawn") != (out->nproc > 0))
+    return usage_error("--bootstrap spawn and --nproc N go together", err, errlen);
   if (input.size() >= sizeof(out->input) || output.size() >= sizeof(out->output))
     return usage_error("path too long", err, errlen);
   copy_str(out->input, sizeof(out->input), input);

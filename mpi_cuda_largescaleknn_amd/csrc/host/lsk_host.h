@@ -35,7 +35,10 @@ typedef struct lsk_cli_args {
   char device[16];    // --device {auto,cuda,cpu}
   char stats[4096];   // --stats <file.json>
   int verbose;        // -v / --verbose
-  int leaf_size;      // --leaf-size (reserved; 64)
+  char bootstrap[16]; // --bootstrap {auto,env,mpi,spawn}: where rank/size come from
+  int nproc;          // --nproc N: ranks started by --bootstrap spawn (0 = unset)
+  char device_map[256];  // --device-map 0,1,...: local rank i uses GPU map[i % len]
+  char balance[8];    // --balance {auto,on,off}: prePartitioned load rebalancing
 } lsk_cli_args;
 
 int lsk_cli_parse(int variant, int argc, const char **argv, lsk_cli_args *out, char *err,

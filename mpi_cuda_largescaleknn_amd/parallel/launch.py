@@ -52,22 +52,59 @@ def _env_int(*names, default=None):
     return default
 
 
+_RANK_VARS = {
+    "env": (("RANK",), ("WORLD_SIZE",), ("LOCAL_RANK",)),
+    "mpi": (("PMI_RANK", "OMPI_COMM_WORLD_RANK", "PMIX_RANK"), ("PMI_SIZE", "OMPI_COMM_WORLD_SIZE"),
+            ("MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK")),
+}
+
+
+def rank_info(bootstrap: str = "auto") -> tuple[int, int, int]:
+    """(rank, size, local rank) from the launcher's environment: torchrun / spawn
+    (`env`: RANK, WORLD_SIZE, LOCAL_RANK), MPICH / Open MPI / PMIx (`mpi`), or either
+    (`auto`, torchrun variables first)."""
+    if bootstrap == "auto":
+        names = [sum(v, ()) for v in zip(_RANK_VARS["env"], _RANK_VARS["mpi"])]
+    elif bootstrap in _RANK_VARS:
+        names = list(_RANK_VARS[bootstrap])
+    else:
+        raise ValueError(f"bootstrap must be auto, env or mpi, not {bootstrap!r}")
+    rank = _env_int(*names[0], default=0)
+    size = _env_int(*names[1], default=1)
+    local = _env_int(*names[2], default=rank)
+    if not (0 <= rank < size):
+        raise ValueError(f"bad rank {rank} of {size} from the {bootstrap} bootstrap")
+    return rank, size, local
+
+
+def pick_device(rank: int, local: int, ndev: int, gpu_affinity: int = 0,
+                device_map: list[int] | None = None) -> int:
+    """GPU of this rank: --device-map [local % len] if given, else the reference's
+    -g G (rank % G, unorderedDataVariant.cu:138-143), else the local rank (fixes D9)."""
+    if device_map:
+        return device_map[local % len(device_map)]
+    if gpu_affinity:
+        return rank % gpu_affinity
+    return local % max(1, ndev)
+
+
 def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False,
-         force_distributed: bool | None = None) -> Launch:
+         force_distributed: bool | None = None, bootstrap: str = "auto",
+         device_map: list[int] | None = None) -> Launch:
     """Bootstrap this rank. `force_distributed` (default: env LSKNN_FORCE_DIST=1) builds a
     process group and the multi-rank pipeline even for a single rank, so that a 1-GPU run
     executes every collective through RCCL."""
     if force_distributed is None:
         force_distributed = os.environ.get("LSKNN_FORCE_DIST", "0") == "1"
-    rank = _env_int("RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "PMIX_RANK", default=0)
-    size = _env_int("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
-    local = _env_int("LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", default=rank)
+    rank, size, local = rank_info("auto" if bootstrap == "spawn" else bootstrap)
     use_gpu = device_pref != "cpu" and torch.cuda.is_available()
     if device_pref == "cuda" and not torch.cuda.is_available():
         raise RuntimeError("--device cuda requested but no GPU is available")
     if use_gpu:
         ndev = torch.cuda.device_count()
-        dev_id = rank % gpu_affinity if gpu_affinity else local % max(1, ndev)
+        dev_id = pick_device(rank, local, ndev, gpu_affinity, device_map)
+        if not 0 <= dev_id < ndev:
+            raise ValueError(f"rank {rank}: GPU {dev_id} does not exist ({ndev} visible)")
         if gpu_affinity:
             print(f"#{rank}/{size}setting active GPU #{dev_id}", flush=True)
         torch.cuda.set_device(dev_id)
@@ -102,6 +139,31 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
     else:
         comm = SingleComm(device)
     return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
+
+
+def spawn_local(nproc: int, module: str, argv: list[str]) -> int:
+    """--bootstrap spawn: start `nproc` local ranks of `python -m module argv...` (each
+    with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* set, bootstrap env) and wait for them.
+    Called before anything touches the GPU. A failing rank's peers abort through the
+    watchdog; the launcher returns the first non-zero exit code."""
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-m", module, *argv, "--bootstrap", "env"], env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        rc = rc or code
+    return rc
 
 
 def finalize(launch: Launch) -> None:

@@ -349,11 +349,24 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     return res
 
 
+IMBALANCE_LIMIT = 1.2  # --balance auto: rebalance when max/mean points per rank exceeds it
+
+
 def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
-                       info: RunInfo | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+                       info: RunInfo | None = None, out: torch.Tensor | None = None,
+                       balance: str = "auto") -> torch.Tensor:
     """k-th-NN distance of every local point (input order) when each rank holds one
     (spatially coherent) input file (reference prePartitionedData variant). `out` as in
-    unordered_knn (on one rank a pinned host tensor is written by the kernel directly)."""
+    unordered_knn (on one rank a pinned host tensor is written by the kernel directly).
+
+    Skewed file sets: the reference serves a hot rank's whole shard to
+    every requester (prePartitionedDataVariant.cu:337-344) and its own queries stay on
+    it. With balance="on" — or "auto" when max/mean points per rank > IMBALANCE_LIMIT —
+    the files go through the unordered pipeline instead (count-balanced spatial
+    redistribution, halo, return): every rank owns ~N/P points and each file's results
+    still come back in its own order."""
+    if balance not in ("auto", "on", "off"):
+        raise ValueError(f"balance must be auto, on or off, not {balance!r}")
     info = info or RunInfo(PhaseTimer(False, points.device))
     info.timer.start()
     points = points.contiguous()
@@ -361,9 +374,13 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     if not comm.distributed:
         n_total = n_local
     else:
-        t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
-        comm.allreduce_(t, "sum")
-        n_total = int(t.item())
+        counts = comm.allgather(torch.tensor([n_local], dtype=torch.int64, device=comm.device)).view(-1).cpu()
+        n_total = int(counts.sum())
+        ratio = float(counts.max()) * comm.size / max(n_total, 1)
+        info.counts["imbalance_x1000"] = int(round(ratio * 1000))
+        if balance == "on" or (balance == "auto" and ratio > IMBALANCE_LIMIT):
+            info.counts["rebalanced"] = 1
+            return unordered_knn(points, comm, cfg, info, n_total=n_total, out=out)
     box = K.bounds(points)
     gbox = global_box(points, comm) if comm.distributed else box
     hint2 = E.radius_hint(gbox, n_total, cfg.k)

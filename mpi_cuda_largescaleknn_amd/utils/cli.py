@@ -8,7 +8,9 @@ last positional argument wins; `-k` >= 1, `-o` and the positional are required; 
 other dash-argument is an error; on error the reference's stderr text is printed and
 the process exits with 1. Extensions (long options only, defaults unchanged):
 ``--mode {auto,halo,ring,peer}``, ``--device {auto,cuda,cpu}``, ``--stats <json>``,
-``-v/--verbose``.
+``-v/--verbose``, ``--bootstrap {auto,env,mpi,spawn}`` (+ ``--nproc N`` for spawn: the
+launcher starts N local ranks itself), ``--device-map 0,1,..`` (local rank -> GPU) and
+``--balance {auto,on,off}`` (prePartitioned: spatial rebalancing of skewed files).
 """
 from __future__ import annotations
 
@@ -33,6 +35,10 @@ class Args:
     device: str
     stats: str
     verbose: bool
+    bootstrap: str = "auto"
+    nproc: int = 0
+    device_map: list | None = None
+    balance: str = "auto"
 
 
 class UsageError(Exception):
@@ -62,6 +68,10 @@ def parse(variant: int, argv: list[str]) -> Args:
         device=out.device.decode(),
         stats=out.stats.decode(),
         verbose=bool(out.verbose),
+        bootstrap=out.bootstrap.decode(),
+        nproc=int(out.nproc),
+        device_map=[int(x) for x in out.device_map.decode().split(",")] if out.device_map else None,
+        balance=out.balance.decode(),
     )
 
 

@@ -91,3 +91,56 @@ def test_rank_count_must_match_file_list(data):
     p = run([PRE, str(lst), "-o", str(data / "x"), "-k", "5", "--device", "cpu"], nproc=3, check=False)
     assert p.returncode != 0
     assert "number of input files does not match MPI size" in p.stderr
+
+
+def test_bootstrap_spawn_matches_single(data):
+    """--bootstrap spawn --nproc 3: the launcher starts its own 3 local ranks (no torchrun)."""
+    out = data / "spawn.float"
+    p = run([UN, str(data / "pts.float3"), "-o", str(out), "-k", "20", "--device", "cpu",
+             "--bootstrap", "spawn", "--nproc", "3"])
+    assert "#2/3: got" in p.stdout
+    assert out.read_bytes() == (data / "ref.float").read_bytes()
+
+
+def test_prepartitioned_spawn_balance_on(data, tmp_path):
+    pts = io.read_points(str(data / "pts.float3"))
+    names = []
+    for r, (b, e) in enumerate([(0, 9000), (9000, 10000), (10000, 12000)]):  # skewed files
+        f = tmp_path / f"part{r}.float3"
+        io.write_points(str(f), pts[b:e])
+        names.append(str(f))
+    (tmp_path / "list.txt").write_text("\n".join(names) + "\n")
+    run([PRE, str(tmp_path / "list.txt"), "-o", str(tmp_path / "out"), "-k", "20", "--device", "cpu",
+         "--bootstrap", "spawn", "--nproc", "3", "--balance", "on"])
+    got = b"".join((tmp_path / f"out_{r:06d}.float").read_bytes() for r in range(3))
+    assert got == (data / "ref.float").read_bytes()
+
+
+@pytest.mark.parametrize("bad,msg", [(["--bootstrap", "slurm"], "invalid --bootstrap"),
+                                     (["--nproc", "2"], "go together"),
+                                     (["--device-map", "0,,1"], "invalid --device-map"),
+                                     (["--balance", "yes"], "invalid --balance")])
+def test_extension_flag_errors(data, bad, msg):
+    p = run([UN, str(data / "pts.float3"), "-o", "x.float", "-k", "4"] + bad, check=False)
+    assert p.returncode == 1 and msg in p.stderr
+
+
+def test_device_map_and_bootstrap_env():
+    from mpi_cuda_largescaleknn_amd.parallel import launch as L
+
+    assert L.pick_device(5, 1, 8, 0, [3, 2]) == 2
+    assert L.pick_device(5, 1, 8, 4, None) == 1       # reference -g: rank % G
+    assert L.pick_device(5, 1, 8, 0, None) == 1       # local rank
+    env = {"PMI_RANK": "2", "PMI_SIZE": "4", "RANK": "0", "WORLD_SIZE": "1"}
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update(env)
+        assert L.rank_info("mpi")[:2] == (2, 4)
+        assert L.rank_info("env")[:2] == (0, 1)
+        assert L.rank_info("auto")[:2] == (0, 1)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v

@@ -104,3 +104,45 @@ def test_bucket_tree_cpu_invariants():
     # perm is a permutation and pts are the permuted input
     assert torch.equal(torch.sort(idx.perm.long()).values, torch.arange(n))
     assert torch.equal(idx.pts[:n], p[idx.perm.long()])
+
+
+def _fp64_kth(p, k, r=math.inf, chunk=512):
+    """Independent float64 brute force (PyTorch): k-th smallest true squared distance
+    among points with d2 < r^2 (self counted), r^2 if fewer than k qualify."""
+    pd = p.double()
+    r2 = r * r
+    out = torch.empty(p.shape[0], dtype=torch.float64)
+    for s in range(0, p.shape[0], chunk):
+        q = pd[s:s + chunk]
+        d2 = ((q[:, None, :] - pd[None, :, :]) ** 2).sum(-1)
+        d2 = torch.where(d2 < r2, d2, torch.full_like(d2, math.inf))
+        kth = torch.kthvalue(d2, min(k, d2.shape[1]), dim=1).values
+        out[s:s + chunk] = torch.where(torch.isinf(kth), torch.full_like(kth, r2), kth)
+    return out
+
+
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_oracle_against_fp64_brute_force_20k(k):
+    """The C++ oracle (fp32 canonical d2) agrees with an fp64 PyTorch brute force on 20K
+    points to within the rounding of fp32 d2 (a few ulp)."""
+    p = uniform(20000, seed=21)
+    got = K.kth_cpu(p, p, k, math.inf, "kdtree").double()
+    ref = _fp64_kth(p, k)
+    rel = ((got - ref).abs() / ref.clamp_min(1e-30))
+    assert float(rel.max()) < 5e-7, float(rel.max())
+
+
+@pytest.mark.parametrize("k,r", [(7, math.inf), (27, math.inf), (30, 0.13), (200, 0.1)])
+def test_oracle_against_fp64_lattice_ties_and_cutoff(k, r):
+    """Lattice points (coordinates j/16, every d2 exact in fp32): massive ties; the fp32
+    oracle must equal the fp64 brute force exactly, also with a -r cutoff."""
+    p = lattice(16)
+    got = K.kth_cpu(p, p, k, E.cut2_of(r), "kdtree").double()
+    ref = _fp64_kth(p, k, r)
+    if math.isinf(r):
+        assert torch.equal(got, ref)
+    else:
+        # cutoff: same set of outputs; the "fewer than k" value is fp32(r)^2 in fp32
+        short = ref == r * r
+        assert torch.equal(got[~short], ref[~short])
+        assert torch.all(got[short] == float(E.cut2_of(r)))

@@ -249,3 +249,25 @@ def test_cmake_build_and_ctest(tmp_path):
         assert r.returncode == 0, f"{' '.join(cmd)} failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
     assert os.path.exists(os.path.join(b, "liblsknn_hip.so"))
     assert os.path.exists(os.path.join(b, "liblsknn_host.so"))
+
+
+def test_cmake_sanitized_host_ctest(tmp_path):
+    """the host runtime and its unit tests built with
+    -DLSKNN_SANITIZE=address;undefined pass CTest (CPU code only)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("cmake") is None or shutil.which("ninja") is None:
+        pytest.skip("cmake/ninja not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    b = str(tmp_path / "build_san")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1")
+    for cmd in (["cmake", "-S", root, "-B", b, "-G", "Ninja", "-DLSKNN_SANITIZE=address;undefined",
+                 "-DCMAKE_BUILD_TYPE=RelWithDebInfo"],
+                ["cmake", "--build", b, "-j8", "--target", "lsknn_host_tests"],
+                ["ctest", "--test-dir", b, "--output-on-failure"]):
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, f"{' '.join(cmd)} failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    flags = open(os.path.join(b, "build.ninja")).read()
+    assert "-fsanitize=address,undefined" in flags

@@ -209,3 +209,30 @@ def test_unordered_loopback_sub_cell_core(size):
 
     out = torch.cat(run_loopback(size, fn))
     assert torch.equal(out, oracle(p, k))
+
+
+@pytest.mark.parametrize("balance", ["auto", "off", "on"])
+def test_prepartitioned_skewed_files_rebalance(balance):
+    """8 spatial files, one holding half of the points: the balanced run
+    gives every rank ~N/8 points to query, the results stay exact and in file order."""
+    size = 8
+    p = uniform(16000, seed=12)
+    k = 10
+    cfg = E.KnnConfig(k=k, publish_levels=4)
+    # x < 0.5 -> rank 0 (half the points), the rest in 7 slabs
+    owner = torch.where(p[:, 0] < 0.5, torch.zeros_like(p[:, 0]).long(),
+                        1 + torch.clamp(((p[:, 0] - 0.5) * 14).long(), max=6))
+    parts = [p[owner == r] for r in range(size)]
+    infos = [PL.RunInfo(PL.PhaseTimer(False, torch.device("cpu"))) for _ in range(size)]
+    outs = run_loopback(size, lambda c: PL.prepartitioned_knn(parts[c.rank], c, cfg, infos[c.rank],
+                                                              balance=balance))
+    ref = oracle(p, k)
+    for r in range(size):
+        assert torch.equal(outs[r], ref[owner == r])
+    owned = [i.counts["owned_points"] for i in infos]
+    assert sum(owned) == 16000
+    if balance == "off":
+        assert max(owned) == parts[0].shape[0] and all("rebalanced" not in i.counts for i in infos)
+    else:
+        assert all(i.counts.get("rebalanced") == 1 for i in infos)
+        assert max(owned) < 1.1 * 16000 / size, owned
