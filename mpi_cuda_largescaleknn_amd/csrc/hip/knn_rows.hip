@@ -63,6 +63,16 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_TOP_BINS
 #define LSK_TOP_BINS 16
 #endif
+// replay re-tests the logged quarters' boxes (per logged row) against the current
+// bounds instead of appending every logged quarter
+#ifndef LSK_REPLAY_RETEST
+#define LSK_REPLAY_RETEST 0
+#endif
+// prune the pass-1 log: (quarter, row) pairs whose pass-1 processing found no value below
+// any lane's bound are dropped before the collect / later replays
+#ifndef LSK_LOG_PRUNE
+#define LSK_LOG_PRUNE 1
+#endif
 // per-candidate wave-uniform skip of the bin update (0.154 vs 0.159 s, same data)
 #ifndef LSK_HIST_SKIP
 #define LSK_HIST_SKIP 1
@@ -135,6 +145,10 @@ struct Lane {
   uint32_t band_lo, band_w, m, bc;
   uint32_t coff, ccnt;
   uint32_t ans;
+#ifdef LSK_PROFILE
+  uint32_t pdead, pslots;  // HIST candidate slots with no lane in range / all slots
+  bool pband;              // COLLECT: this lane had a value in its band this step
+#endif
 };
 
 // Histogram range [lo_b, hi_b) in 64 bins of 2^shift float bits. Values below lo_b are
@@ -196,6 +210,16 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
 #pragma unroll
   for (int t = 1; t < G; t++) umin = min(umin, u[t]);
   const bool lane_in = umin < s.hi_b;  // (profiling: this lane had a value in range)
+#ifdef LSK_PROFILE
+  if (MODE == MODE_HIST) {
+#pragma unroll
+    for (int t = 0; t < G; t++) s.pdead += __ballot(u[t] < s.hi_b) == 0 ? 1u : 0u;
+    s.pslots += G;
+  } else {
+#pragma unroll
+    for (int t = 0; t < G; t++) s.pband = s.pband || (u[t] - s.band_lo < s.band_w);
+  }
+#endif
   if (MODE == MODE_HIST) {
     if (!__ballot(lane_in)) return false;
     // bin = sat(v - lo_b) >> shift (< 64 for every v < hi_b); bins 2j, 2j+1 share the
@@ -318,6 +342,14 @@ struct WaveCtx {
   // 4 row bits per quarter) held by lane n % 64 of word n / 64 of two private arrays
   uint32_t logn;
   bool logging, log_ok;
+#if LSK_LOG_PRUNE
+  // pass-1 "dead row-step" stream: bit h of row r (lane 16r + h/32, bit h%32) is set when
+  // the row's h-th queue entry gave no lane of the row a value below its bound; after
+  // pass 1 those (quarter, row) pairs are removed from the log (they cannot hold a value
+  // below any later bound or inside the collect band: bounds only shrink)
+  uint32_t *dead;  // private (scratch) word: keeps the stream out of the VGPR budget
+  uint32_t nseed;  // seed quarters appended to every row before the logged ones
+#endif
   uint32_t *logq, *logm;
   const float *p0, *p1, *pdef;  // tree point arrays (pdef: one that is non-empty)
   uint32_t n0, n1;
@@ -325,6 +357,7 @@ struct WaveCtx {
 #ifdef LSK_PROFILE
   uint64_t prof[8];
   uint32_t prof_rows_entry, prof_rows_in;  // pass-1 row-steps with an entry / with a value in range
+  uint32_t prof_crows_entry, prof_crows_in;  // collect row-steps with an entry / with a band value
 #endif
   uint32_t steps, quarters, nodes_visited, csteps, cnodes;
 };
@@ -390,6 +423,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
   const float inf = __builtin_inff();
   for (uint32_t st = 0; st < n; st++) {
     const uint32_t ccnt = cnt;
+    const uint32_t hcur = W.rhead;  // queue position of the entry processed by this step
     const bool live = (uint32_t)(W.lane & 15) < ccnt;
     const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
     W.rhead += W.rhead < W.rlen ? 1u : 0u;
@@ -397,14 +431,30 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
 #ifdef LSK_PROFILE
+    s.pband = false;
+#endif
     const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+#ifdef LSK_PROFILE
     if (MODE == MODE_HIST) {
       const uint32_t re = row_bits(__ballot(ccnt > 0u)), ri = row_bits(__ballot(lin));
       W.prof_rows_entry += __popc(re);
       W.prof_rows_in += __popc(re & ri);
+    } else {
+      const uint32_t re = row_bits(__ballot(ccnt > 0u)), ri = row_bits(__ballot(s.pband));
+      W.prof_crows_entry += __popc(re);
+      W.prof_crows_in += __popc(re & ri);
+    }
+#endif
+#if LSK_LOG_PRUNE
+    if (MODE == MODE_HIST && W.logging) {
+      const uint32_t rin = row_bits(__ballot(lin)), rent = row_bits(__ballot(ccnt > 0u));
+      const uint32_t dead = ((rent & ~rin) >> W.row) & 1u;
+      if (dead && hcur < 512u && (uint32_t)(W.lane & 15) == (hcur >> 5))
+        W.dead[hcur >> 9] |= 1u << (hcur & 31u);  // (index 0: dynamic, so it stays in scratch)
     }
 #else
-    process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+    (void)lin;
+    (void)hcur;
 #endif
   }
   W.hd0 = min(W.hd0 + n, W.len0);
@@ -555,6 +605,48 @@ __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preservi
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(v));
 }
 
+#if LSK_LOG_PRUNE
+// Drop from the pass-1 log every (quarter, row) pair whose pass-1 step gave no lane of the
+// row a value below its bound (WaveCtx::dead). Row r's queue held the seeds first, then
+// the logged quarters in log order (quarter order inside an entry), so the stream index
+// of a logged pair is nseed + (row-r pairs in earlier entries) + (row-r pairs of earlier
+// quarters of the same entry). One 64-entry log word per iteration, all lanes at once.
+__device__ void log_prune(WaveCtx &W) {
+  uint32_t base01 = 0, base23 = 0;  // row pairs before this word (rows 0|1, 2|3: 16-bit fields)
+  const uint32_t dw = W.dead[0];
+#pragma unroll 1
+  for (uint32_t w = 0; w < kLogWords; w++) {
+    if ((w << 6) >= W.logn) break;
+    const bool have = (w << 6) + (uint32_t)W.lane < W.logn;
+    const uint32_t mk = have ? W.logm[w] : 0u;
+    const uint32_t c01 = __popc(mk & 0x11111111u) | (__popc(mk & 0x22222222u) << 16);
+    const uint32_t c23 = __popc(mk & 0x44444444u) | (__popc(mk & 0x88888888u) << 16);
+    uint32_t x01 = c01, x23 = c23;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y01 = __shfl_up(x01, o), y23 = __shfl_up(x23, o);
+      if (W.lane >= o) {
+        x01 += y01;
+        x23 += y23;
+      }
+    }
+    const uint32_t e01 = base01 + x01 - c01, e23 = base23 + x23 - c23;  // exclusive
+    uint32_t keep = mk;
+#pragma unroll 1
+    for (uint32_t b = 0; b < 32; b++) {  // bit b: quarter b / 4, row b % 4
+      const uint32_t r = b & 3u;
+      const uint32_t prev = ((r < 2u ? e01 : e23) >> (16u * (r & 1u))) & 0xffffu;
+      const uint32_t idx = W.nseed + prev + (uint32_t)__popc(mk & (0x11111111u << r) & ((1u << b) - 1u));
+      const uint32_t word = (uint32_t)__shfl((int)dw, (int)(16u * r + min(idx >> 5, 15u)));
+      if (((mk >> b) & 1u) && idx < 512u && ((word >> (idx & 31u)) & 1u)) keep &= ~(1u << b);
+    }
+    if (have) W.logm[w] = keep;
+    base01 += (uint32_t)__shfl((int)x01, 63);
+    base23 += (uint32_t)__shfl((int)x23, 63);
+  }
+}
+#endif
+
 // Tree walk (wave-uniform DFS, near child first) building the per-row quarter lists,
 // alternating with lockstep processing of what every row has pending (one processing
 // call site per pass keeps the kernel's register allocation tight).
@@ -588,7 +680,14 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   uint32_t fill_rounds = 0;
   Pend P{0, 0, 0, 0, 0, ~0u, ~0u, ~0u, ~0u};  // pending pre-leaf nodes
   uint32_t ri = 0, lq = 0, lmk = 0;  // replay cursor, cached log words
-  if (!replay && W.logging) W.logn = 0;
+  bool force_flush = false;           // replay: a tree switch needs the batch flushed
+  if (!replay && W.logging) {
+    W.logn = 0;
+#if LSK_LOG_PRUNE
+    W.dead[0] = 0;
+    W.nseed = 0;
+#endif
+  }
   while (!finished) {
     bool overflow = false;
     if (++fill_rounds > kGuardRounds) {  // watchdog: never spin on the GPU
@@ -599,7 +698,9 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     for (;;) {
       // room for the pending batch (8 entries per node per row) plus one more node
       const bool room_short = max_pend(W) + 8u * (P.n + 1u) > W.rcap;
-      if (P.n && (P.n == kPend || room_short || (started && sp == 0))) {
+      if (P.n && (P.n == kPend || room_short || (started && sp == 0) || force_flush ||
+                  (replay && ri >= W.logn))) {
+        force_flush = false;
         LSK_PT(tq0);  // the one flush site (keeps a single inlined copy)
         flush_pending<MODE>(s, W, T.qnodes, t, P, nquarters, skip_lo, skip_hi, 32u << depth);
         LSK_PADD(W.prof[4], tq0);
@@ -640,7 +741,12 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
           if (b < 0 || b >= (int64_t)nbuckets) continue;
           for (uint32_t qq = 0; qq < 4; qq++) {
             const uint32_t qid = (uint32_t)b * 4 + qq;
-            if (qid < nquarters) rows_append(W, 0xfu, qid);
+            if (qid < nquarters) {
+              rows_append(W, 0xfu, qid);
+#if LSK_LOG_PRUNE
+              if (!replay) W.nseed++;
+#endif
+            }
           }
         }
         seed_d = seed_d < W.seed ? seed_d + 1 : -1;
@@ -657,10 +763,44 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         }
         const uint32_t e = __builtin_amdgcn_readlane(lq, (int)(ri & 63u));
         const uint32_t mk = __builtin_amdgcn_readlane(lmk, (int)(ri & 63u));
+        const uint32_t tq = e & 0x80000000u, q0 = e & 0x7fffffffu;
+#if LSK_REPLAY_RETEST
+        // re-test the logged quarters against the lanes' current bounds (a shell in the
+        // collect pass) with the logged rows as the mask: same batched box loads as a walk
+        {
+          const uint32_t et = tq >> 31;
+          if (et != t) {
+            if (P.n) {  // flush the other tree's batch first (top of the fill loop)
+              force_flush = true;
+              continue;
+            }
+            t = et;
+            T = pick_tree(A, t);
+            depth = T.depth;
+            nquarters = (uint32_t)((T.n + 15) / 16);
+            skip_lo = 1;
+            skip_hi = 0;
+            if (t == 0 && W.seed > 0) {
+              skip_lo = (int64_t)W.g - W.seed;
+              skip_hi = (int64_t)W.g + W.seed;
+            }
+          }
+          P.p0 = P.n == 0 ? q0 : P.p0;
+          P.p1 = P.n == 1 ? q0 : P.p1;
+          P.p2 = P.n == 2 ? q0 : P.p2;
+          P.p3 = P.n == 3 ? q0 : P.p3;
+          P.m0 = P.n == 0 ? mk : P.m0;
+          P.m1 = P.n == 1 ? mk : P.m1;
+          P.m2 = P.n == 2 ? mk : P.m2;
+          P.m3 = P.n == 3 ? mk : P.m3;
+          P.n++;
+          ri++;
+          continue;
+        }
+#else
         // the logged rows per quarter are appended as they are: they are a superset of
         // what any later pass needs (bounds only shrink), and skipping the re-test keeps
         // replay free of box loads
-        const uint32_t tq = e & 0x80000000u, q0 = e & 0x7fffffffu;
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
           const uint32_t rm = (mk >> (4 * j)) & 0xfu;
@@ -668,6 +808,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         }
         ri++;
         continue;
+#endif
       }
       if (sp == 0) {  // (nothing pending here: flushed above)
         t++;
@@ -873,6 +1014,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   uint32_t logq[kLogWords], logm[kLogWords];  // private (scratch) pass-1 log
   W.logq = logq;
   W.logm = logm;
+#if LSK_LOG_PRUNE
+  uint32_t deadw[2];  // private dead-row-step stream word (WaveCtx::dead)
+  W.dead = deadw;
+#endif
   W.logn = 0;
   W.logging = W.log_ok = false;
   W.p0 = A.tree[0].pts;
@@ -884,6 +1029,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 #ifdef LSK_PROFILE
   for (int i = 0; i < 8; i++) W.prof[i] = 0;
   W.prof_rows_entry = W.prof_rows_in = 0;
+  W.prof_crows_entry = W.prof_crows_in = 0;
   LSK_PT(twave0);
 #endif
   W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
@@ -944,6 +1090,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   s.c_base = 0;
   s.nudf = 0;
   s.ans = cut_b;
+#ifdef LSK_PROFILE
+  s.pdead = s.pslots = 0;
+  s.pband = false;
+#endif
 
   int64_t total_pts = 0;
   for (int t = 0; t < A.ntrees; t++) total_pts += pick_tree(A, t).n;
@@ -1014,6 +1164,9 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       else
         traverse<MODE_HIST, false, NT>(s, W, A);
       LSK_PADD(W.prof[2], tt0);
+#if LSK_LOG_PRUNE
+      if (W.logging && W.log_ok) log_prune(W);
+#endif
       W.logging = false;
       first = false;
       bool ovf = false;
@@ -1164,6 +1317,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   if (A.stats && lane == 0) {
     atomicAdd(&A.stats[24], (unsigned long long)W.prof_rows_entry);
     atomicAdd(&A.stats[25], (unsigned long long)W.prof_rows_in);
+    atomicAdd(&A.stats[28], (unsigned long long)s.pdead);
+    atomicAdd(&A.stats[29], (unsigned long long)s.pslots);
+    atomicAdd(&A.stats[30], (unsigned long long)W.prof_crows_entry);
+    atomicAdd(&A.stats[31], (unsigned long long)W.prof_crows_in);
   }
 #endif
   if (A.stats) {

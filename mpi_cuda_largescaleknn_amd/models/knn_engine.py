@@ -78,7 +78,8 @@ class KnnStats:
                  # cycle profile (LSK_PROFILE kernel builds only)
                  "prof_proc_hist", "prof_proc_collect", "prof_walk_hist", "prof_walk_collect",
                  "prof_quarters", "prof_inner_nodes", "prof_select", "prof_wave",
-                 "prof_rows_entry", "prof_rows_in", "failed_lanes", "binovf_lanes"]
+                 "prof_rows_entry", "prof_rows_in", "failed_lanes", "binovf_lanes",
+                 "prof_dead_slots", "prof_slots", "prof_crows_entry", "prof_crows_in"]
         vals = raw.cpu().tolist()
         for i, nm in enumerate(names):
             self.counters[nm] = self.counters.get(nm, 0) + int(vals[i])
