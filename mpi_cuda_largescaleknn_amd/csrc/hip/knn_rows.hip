@@ -611,7 +611,17 @@ __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preservi
 // the logged quarters in log order (quarter order inside an entry), so the stream index
 // of a logged pair is nseed + (row-r pairs in earlier entries) + (row-r pairs of earlier
 // quarters of the same entry). One 64-entry log word per iteration, all lanes at once.
-__device__ void log_prune(WaveCtx &W) {
+#ifndef LSK_PRUNE_NOINLINE
+#define LSK_PRUNE_NOINLINE 1
+#endif
+#if LSK_PRUNE_NOINLINE
+// (an out-of-line call: WaveCtx then lives in scratch and the compiler keeps only its hot
+// fields in registers, which measured faster than the all-register allocation — 1e8
+// k=100: 0.138 vs 0.149 s; profiles/r2_kernel)
+__device__ __attribute__((noinline)) void log_prune(WaveCtx &W) {
+#else
+__device__ __forceinline__ void log_prune(WaveCtx &W) {
+#endif
   uint32_t base01 = 0, base23 = 0;  // row pairs before this word (rows 0|1, 2|3: 16-bit fields)
   const uint32_t dw = W.dead[0];
 #pragma unroll 1
@@ -984,6 +994,11 @@ __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *p
   return sum == s.c_hi;
 }
 
+#ifdef LSK_W_ESCAPE
+// tuning experiment: make WaveCtx escape to memory without the log prune
+__device__ __attribute__((noinline)) void w_escape(WaveCtx &W) { asm volatile("" ::"v"(W.k)); }
+#endif
+
 template <int RCAP, int NT>
 __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_rows_kernel(const lsk_knn_args A) {
   __shared__ WaveLdsR<RCAP> lds[kWavesPerBlock];
@@ -1033,6 +1048,9 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   LSK_PT(twave0);
 #endif
   W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
+#ifdef LSK_W_ESCAPE
+  w_escape(W);
+#endif
 
   Lane s;
   s.qx = valid ? A.qpts[3 * qi] : 0.f;
