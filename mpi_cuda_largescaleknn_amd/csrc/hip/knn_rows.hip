@@ -78,6 +78,13 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_REPLAY_RETEST
 #define LSK_REPLAY_RETEST 0
 #endif
+// best-first walk: inner nodes popped in order of their box distance to the centre of the
+// wave's queries (2; 1 = to the wave's query box) from a 64-entry priority list in two
+// VGPRs, DFS stack as bounded overflow, instead of DFS ordered by the bucket-index gap
+// (0). 1e8 uniform, k=100: DFS 0.135 s, box key 0.129 s, centre key 0.126 s.
+#ifndef LSK_BEST_FIRST
+#define LSK_BEST_FIRST 2
+#endif
 // walk/process alternation: the walk fills the row queues until every row has this
 // many entries pending (then one lockstep drain)
 #ifndef LSK_FILL_MIN
@@ -699,6 +706,38 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   // DFS stack in one VGPR (lane i = entry i; < 64 entries): v_readlane to pop, a
   // lane select to push, instead of an LDS round trip per node
   uint32_t stk = 0;
+#if LSK_BEST_FIRST
+  // priority list: lane i holds (node, key) entry i; empty = (any, +inf); npq entries
+  uint32_t pqn = 0u;
+  float pqk = __builtin_inff();
+  uint32_t npq = 0;
+  const lsk::box3f wbox{{W.wlx, W.wly, W.wlz}, {W.whx, W.why, W.whz}};
+  // a node popped from the DFS stack pushes its children back onto the stack (depth-first
+  // inside an overflowed subtree), and the stack is drained before the list is popped
+  // again: the stack then never holds more than 4 + 3 per level entries (< 64), while
+  // the list holds at most 64
+  bool dfs_mode = false;
+  auto pq_push = [&](uint32_t cn, lsk::v4f lo, lsk::v4f hi) {
+    if (!dfs_mode && npq < 64u) {
+#if LSK_BEST_FIRST == 2
+      // key: squared distance from the wave's query-box centre to the node box
+      const float key = lsk::uniform_f(lsk::box_dist2(c, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}));
+#else
+      // key: squared distance between the wave's query box and the node box
+      const float key = lsk::uniform_f(lsk::box_box_dist2(wbox, {{lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}}));
+#endif
+      const uint64_t fr = __ballot(pqk == __builtin_inff());
+      const int l = (int)__builtin_ctzll(fr);
+      if (W.lane == l) {
+        pqn = cn;
+        pqk = key < __builtin_inff() ? key : 3.0e38f;  // never store the empty marker
+      }
+      npq++;
+    } else {
+      stk = W.lane == (int)sp++ ? cn : stk;
+    }
+  };
+#endif
   bool started = false, finished = false;
   int32_t seed_d = W.seed > 0 ? 0 : -1;  // next seed distance (tree 0 only)
   lsk_tree_view T = pick_tree(A, 0);
@@ -726,7 +765,12 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     for (;;) {
       // room for the pending batch (8 entries per node per row) plus one more node
       const bool room_short = max_pend(W) + 8u * (P.n + 1u) > W.rcap;
-      if (P.n && (P.n == kPend || room_short || (started && sp == 0) || force_flush ||
+#if LSK_BEST_FIRST
+      const bool walk_empty = sp == 0 && npq == 0;
+#else
+      const bool walk_empty = sp == 0;
+#endif
+      if (P.n && (P.n == kPend || room_short || (started && walk_empty) || force_flush ||
                   (replay && ri >= W.logn))) {
         force_flush = false;
         LSK_PT(tq0);  // the one flush site (keeps a single inlined copy)
@@ -759,8 +803,16 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
           skip_lo = (int64_t)W.g - W.seed;
           skip_hi = (int64_t)W.g + W.seed;
         }
+#if LSK_BEST_FIRST
+        if (W.lane == 0) {  // the root enters the priority list
+          pqn = 1u;
+          pqk = 0.f;
+        }
+        npq = 1;
+#else
         stk = W.lane == 0 ? 1u : stk;
         sp = 1;
+#endif
         started = true;
       }
       if (t == 0 && seed_d >= 0) {  // seed buckets g, g-1, g+1, g-2, g+2, ... for every row
@@ -838,13 +890,32 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         continue;
 #endif
       }
+#if LSK_BEST_FIRST
+      if (sp == 0 && npq == 0) {  // (nothing pending here: flushed above)
+#else
       if (sp == 0) {  // (nothing pending here: flushed above)
+#endif
         t++;
         started = false;
         continue;
       }
+#if LSK_BEST_FIRST
+      uint32_t node;
+      dfs_mode = sp != 0;
+      if (!dfs_mode) {
+        const float m = lsk::wave_min(pqk);
+        const int l = (int)__builtin_ctzll(__ballot(pqk == m));
+        node = __builtin_amdgcn_readlane(pqn, l);
+        if (W.lane == l) pqk = __builtin_inff();
+        npq--;
+      } else {
+        sp--;
+        node = __builtin_amdgcn_readlane(stk, (int)sp);
+      }
+#else
       sp--;
       const uint32_t node = __builtin_amdgcn_readlane(stk, (int)sp);
+#endif
       W.nodes_visited++;
       if (MODE == MODE_COLLECT) W.cnodes++;
       const int32_t lvl = 31 - __clz(node);
@@ -902,6 +973,14 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
           k3 = korder(g0 + 3u, 3u);
         }
         need = (uint32_t)__builtin_amdgcn_readfirstlane((int)need);
+#if LSK_BEST_FIRST
+        (void)k0; (void)k1; (void)k2; (void)k3;
+        for (uint32_t j = 0; j < 4u; j++)
+          if ((need >> j) & 1u) {
+            const lsk::v4f lo = nodes[2 * (g0 + j)], hi = nodes[2 * (g0 + j) + 1];
+            pq_push(g0 + j, lo, hi);
+          }
+#else
         // sorting network, descending (push far ... near)
 #define LSK_CSWAP(a, b)                 \
   {                                     \
@@ -915,6 +994,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         if ((need >> (k1 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k1 & 3u) : stk;
         if ((need >> (k2 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k2 & 3u) : stk;
         if ((need >> (k3 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k3 & 3u) : stk;
+#endif
       } else {  // binary step onto level depth-1
         const uint32_t c0 = 2 * node, c1 = c0 + 1;
         const lsk::v4f l0 = nodes[2 * c0], h0 = nodes[2 * c0 + 1];
@@ -926,8 +1006,14 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         const bool first0 = t != 0 || W.g < mid;
         const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
         const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
+#if LSK_BEST_FIRST
+        (void)a; (void)bb; (void)na; (void)nbb;
+        if (n0) pq_push(c0, l0, h0);
+        if (n1) pq_push(c1, l1, h1);
+#else
         if (na) stk = W.lane == (int)sp++ ? a : stk;
         if (nbb) stk = W.lane == (int)sp++ ? bb : stk;
+#endif
       }
       LSK_PADD(W.prof[5], tn0);
     }
