@@ -90,6 +90,10 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_FILL_MIN
 #define LSK_FILL_MIN 8
 #endif
+// (0 = off) drain as soon as the longest row queue holds this many entries
+#ifndef LSK_DRAIN_MAX
+#define LSK_DRAIN_MAX 0
+#endif
 // prune the pass-1 log: (quarter, row) pairs whose pass-1 processing found no value below
 // any lane's bound are dropped before the collect / later replays
 #ifndef LSK_LOG_PRUNE
@@ -784,6 +788,11 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         break;
       }
       if (min_pend(W) >= (uint32_t)LSK_FILL_MIN) break;
+#if LSK_DRAIN_MAX
+      // also drain when one row runs far ahead (its queued quarters were tested against
+      // bounds that its own processing would have tightened)
+      if (max_pend(W) >= (uint32_t)LSK_DRAIN_MAX) break;
+#endif
       if (!started) {
         if (t >= (uint32_t)A.ntrees) {
           finished = true;
@@ -1021,7 +1030,12 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     // fill: the steps every row can take; overflow: at least enough to make room for one
     // more node's 8 quarters in the longest queue; end of walk: everything pending
     const uint32_t mxp = max_pend(W), mnp = min_pend(W);
+#if LSK_DRAIN_MAX
+    const uint32_t nsteps = finished ? mxp : overflow ? max(mnp, mxp + 8u - min(mxp + 8u, W.rcap))
+                                                     : max(mnp, (mxp + 1u) >> 1);
+#else
     const uint32_t nsteps = finished ? mxp : overflow ? max(mnp, mxp + 8u - min(mxp + 8u, W.rcap)) : mnp;
+#endif
     LSK_PT(tp0);
     process_steps<MODE, NT>(s, W, A, nsteps);
     LSK_PADD(W.prof[MODE], tp0);

@@ -29,7 +29,7 @@ def cut2_of(max_radius: float) -> float:
         return float(r * r)
 
 
-SEED_BUCKETS = 2  # Morton-neighbour buckets (each side) that seed the first pass
+SEED_BUCKETS = 1  # curve-neighbour buckets (each side) that seed the first pass (1e8 k=100: 0/1/2 -> 0.126/0.125/0.126 s)
 KNN_IMPL = "rows"  # "rows" (production kernel + exact backstop) or "exact" (backstop only)
 DEBUG_FAIL_MOD = 0  # tests: make the rows kernel hand every m-th query to the backstop
 # HIP-graph captures: the failure words of captured launches, checked after a replay
