@@ -640,31 +640,39 @@ __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preservi
 // the logged quarters in log order (quarter order inside an entry), so the stream index
 // of a logged pair is nseed + (row-r pairs in earlier entries) + (row-r pairs of earlier
 // quarters of the same entry). One 64-entry log word per iteration, all lanes at once.
+// 2: log_prune_impl out of line with scalar arguments (WaveCtx stays in registers,
+// the prune's own temporaries do not raise the kernel's register pressure): 0.1245 s;
+// 1: out of line taking WaveCtx& (WaveCtx forced to scratch): 0.127 s; 0: inlined: 0.149 s
 #ifndef LSK_PRUNE_NOINLINE
-#define LSK_PRUNE_NOINLINE 1
+#define LSK_PRUNE_NOINLINE 2
 #endif
-#if LSK_PRUNE_NOINLINE
+#if LSK_PRUNE_NOINLINE == 2
+// out of line with scalar arguments: WaveCtx stays in registers (it is not passed)
+__device__ __attribute__((noinline)) void log_prune_impl(uint32_t *logm, uint32_t logn, uint32_t dw,
+                                                          uint32_t nseed, int lane) {
+#elif LSK_PRUNE_NOINLINE
 // (an out-of-line call: WaveCtx then lives in scratch and the compiler keeps only its hot
 // fields in registers, which measured faster than the all-register allocation — 1e8
 // k=100: 0.138 vs 0.149 s; profiles/r2_kernel)
-__device__ __attribute__((noinline)) void log_prune(WaveCtx &W) {
+__device__ __attribute__((noinline)) void log_prune_impl(uint32_t *logm, uint32_t logn, uint32_t dw,
+                                                          uint32_t nseed, int lane) {
 #else
-__device__ __forceinline__ void log_prune(WaveCtx &W) {
+__device__ __forceinline__ void log_prune_impl(uint32_t *logm, uint32_t logn, uint32_t dw,
+                                               uint32_t nseed, int lane) {
 #endif
   uint32_t base01 = 0, base23 = 0;  // row pairs before this word (rows 0|1, 2|3: 16-bit fields)
-  const uint32_t dw = W.dead[0];
 #pragma unroll 1
   for (uint32_t w = 0; w < kLogWords; w++) {
-    if ((w << 6) >= W.logn) break;
-    const bool have = (w << 6) + (uint32_t)W.lane < W.logn;
-    const uint32_t mk = have ? W.logm[w] : 0u;
+    if ((w << 6) >= logn) break;
+    const bool have = (w << 6) + (uint32_t)lane < logn;
+    const uint32_t mk = have ? logm[w] : 0u;
     const uint32_t c01 = __popc(mk & 0x11111111u) | (__popc(mk & 0x22222222u) << 16);
     const uint32_t c23 = __popc(mk & 0x44444444u) | (__popc(mk & 0x88888888u) << 16);
     uint32_t x01 = c01, x23 = c23;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y01 = __shfl_up(x01, o), y23 = __shfl_up(x23, o);
-      if (W.lane >= o) {
+      if (lane >= o) {
         x01 += y01;
         x23 += y23;
       }
@@ -675,15 +683,24 @@ __device__ __forceinline__ void log_prune(WaveCtx &W) {
     for (uint32_t b = 0; b < 32; b++) {  // bit b: quarter b / 4, row b % 4
       const uint32_t r = b & 3u;
       const uint32_t prev = ((r < 2u ? e01 : e23) >> (16u * (r & 1u))) & 0xffffu;
-      const uint32_t idx = W.nseed + prev + (uint32_t)__popc(mk & (0x11111111u << r) & ((1u << b) - 1u));
+      const uint32_t idx = nseed + prev + (uint32_t)__popc(mk & (0x11111111u << r) & ((1u << b) - 1u));
       const uint32_t word = (uint32_t)__shfl((int)dw, (int)(16u * r + min(idx >> 5, 15u)));
       if (((mk >> b) & 1u) && idx < 512u && ((word >> (idx & 31u)) & 1u)) keep &= ~(1u << b);
     }
-    if (have) W.logm[w] = keep;
+    if (have) logm[w] = keep;
     base01 += (uint32_t)__shfl((int)x01, 63);
     base23 += (uint32_t)__shfl((int)x23, 63);
   }
 }
+#if LSK_PRUNE_NOINLINE == 1
+__device__ __attribute__((noinline)) void log_prune(WaveCtx &W) {
+  log_prune_impl(W.logm, W.logn, W.dead[0], W.nseed, W.lane);
+}
+#else
+__device__ __forceinline__ void log_prune(WaveCtx &W) {
+  log_prune_impl(W.logm, W.logn, W.dead[0], W.nseed, W.lane);
+}
+#endif
 #endif
 
 // Tree walk (wave-uniform DFS, near child first) building the per-row quarter lists,
