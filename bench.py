@@ -149,7 +149,12 @@ def main():
     def _step(phases: bool = args.phases):
         nonlocal info_last
         info = PL.RunInfo(PL.PhaseTimer(phases, device))
-        pts = host_pts.to(device, non_blocking=True)
+        if comm.distributed and args.variant == "unordered" and args.mode == "halo":
+            # several ranks: the redistribution streams the host points to the device in
+            # chunks overlapped with the all-to-all (pipelines.redistribute_stream)
+            pts = host_pts
+        else:
+            pts = host_pts.to(device, non_blocking=True)
         if args.mode == "ring":
             out = RA.ring_knn(pts, comm, cfg, info)
         elif args.mode == "peer":

@@ -44,7 +44,10 @@ def _run(args, launch) -> int:
     cfg = common.config(args)
     info = common.make_info(launch, bool(args.stats) or args.verbose)
     t0 = common.now(launch)
-    dpts = pts.to(launch.device, non_blocking=True)
+    # several GPU ranks (halo mode): the host points stream to the device inside the
+    # redistribution; otherwise one copy up front
+    streamed = args.mode != "ring" and launch.comm.distributed and launch.device.type == "cuda"
+    dpts = pts if streamed else pts.to(launch.device, non_blocking=True)
     if args.mode == "ring":
         out = RA.ring_knn(dpts, launch.comm, cfg, info)
     else:

@@ -48,9 +48,11 @@ class Comm:
         """Returns a tensor of shape [size, *t.shape]."""
         raise NotImplementedError
 
-    def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int]) -> tuple[torch.Tensor, list[int]]:
+    def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int],
+                  recv_counts: Sequence[int] | None = None) -> tuple[torch.Tensor, list[int]]:
         """Rows send[sum(counts[:j]) : sum(counts[:j+1])] go to rank j. Returns
-        (recv rows ordered by source rank, recv counts per source)."""
+        (recv rows ordered by source rank, recv counts per source). `recv_counts`, when the
+        caller knows them (e.g. a result return), saves the count exchange."""
         raise NotImplementedError
 
     def barrier(self) -> None:
@@ -93,7 +95,7 @@ class SingleComm(Comm):
     def allgather(self, t):
         return t.unsqueeze(0).clone()
 
-    def alltoallv(self, send, send_counts):
+    def alltoallv(self, send, send_counts, recv_counts=None):
         return send.clone(), [int(send_counts[0])]
 
     def barrier(self):
@@ -165,9 +167,10 @@ class TorchComm(Comm):
         dist.all_gather(list(out.unbind(0)), t, group=self.group)
         return out
 
-    def alltoallv(self, send, send_counts):
+    def alltoallv(self, send, send_counts, recv_counts=None):
         send_counts = [int(c) for c in send_counts]
-        recv_counts = self.exchange_counts(send_counts)
+        recv_counts = (self.exchange_counts(send_counts) if recv_counts is None
+                       else [int(c) for c in recv_counts])
         row_shape = tuple(send.shape[1:])
         if not self.distributed:
             return send.clone(), recv_counts
@@ -308,7 +311,7 @@ class LoopbackComm(Comm):
         self._sync_device()
         return out
 
-    def alltoallv(self, send, send_counts):
+    def alltoallv(self, send, send_counts, recv_counts=None):
         send_counts = [int(c) for c in send_counts]
         offs = [0]
         for c in send_counts:

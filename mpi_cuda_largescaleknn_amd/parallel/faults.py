@@ -121,8 +121,8 @@ class MonitoredComm(Comm):
     def allgather(self, t):
         return self._call("allgather", t)
 
-    def alltoallv(self, send, send_counts):
-        return self._call("alltoallv", send, send_counts)
+    def alltoallv(self, send, send_counts, recv_counts=None):
+        return self._call("alltoallv", send, send_counts, recv_counts)
 
     def barrier(self):
         return self._call("barrier")

@@ -186,6 +186,134 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
     return recv, recv_counts, perm, send_counts
 
 
+STREAM_CHUNK = 1 << 25  # points per host->device chunk of the streamed redistribution
+
+
+@dataclass
+class Redist:
+    """Bookkeeping of a (streamed) redistribution, for the result return."""
+    owned: torch.Tensor           # [m, 3] points this rank owns (received-row order)
+    ret_index: torch.Tensor       # int64: owned-row order -> return-send order (by dest)
+    ret_counts: list              # rows returned to each rank
+    origin_index: torch.Tensor    # int64: return-receive order -> local input row
+    back_counts: list             # rows coming back from each rank
+    box: torch.Tensor             # global box of all points (exact)
+
+
+def redistribute_stream(host_pts: torch.Tensor, comm: Comm, info: RunInfo,
+                        chunk: int | None = None) -> Redist:
+    """Spatial redistribution fed in chunks straight from host memory: the host->device
+    copies of all chunks are queued on a copy stream up front, and chunk c is keyed,
+    partitioned and sent (all-to-all-v) while chunks c+1.. are still in flight, so the
+    PCIe transfer hides the partitioning and most of the xGMI exchange.
+
+    Ownership uses the cube of the ranks' FIRST chunks (all-reduced) and splitters from
+    their key histogram; points outside that cube get clamped keys. Neither affects
+    exactness (the k-NN is exact for any ownership); they only shape the load balance, so
+    a first chunk that is unrepresentative of the rest (e.g. input sorted in space) costs
+    speed, not correctness. The exact global box is all-reduced after the last chunk."""
+    dev = comm.device
+    n = host_pts.shape[0]
+    gpu = dev.type == "cuda"
+    size = comm.size
+    chunk = max(1, int(chunk or STREAM_CHUNK))
+    spans = [(s, min(s + chunk, n)) for s in range(0, n, chunk)] or [(0, 0)]
+    cur = torch.cuda.current_stream(dev) if gpu else None
+    copy_stream = torch.cuda.Stream(dev) if gpu else None
+    dchunks, events = [], []
+    for s, e in spans:
+        if gpu:
+            d = torch.empty((e - s, 3), dtype=torch.float32, device=dev)  # allocated on `cur`
+            copy_stream.wait_stream(cur)
+            with torch.cuda.stream(copy_stream):
+                d.copy_(host_pts[s:e], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(copy_stream)
+        else:
+            d, ev = host_pts[s:e], None
+        dchunks.append(d)
+        events.append(ev)
+
+    def ready(c):
+        if events[c] is not None:
+            cur.wait_event(events[c])
+        return dchunks[c]
+
+    # ownership cube from every rank's first chunk; exact bounds accumulate per chunk
+    first = ready(0)
+    box0 = global_box(first, comm)
+    lo_hi = K.bounds(first)[0:6].clone()
+    nb = 1 << SPLIT_BITS
+    keys0, _ = K.morton(first, box0, with_iota=False)
+    hist = torch.zeros(nb, dtype=torch.int32, device=dev)
+    if K.is_gpu(keys0):
+        from .. import _native
+        K.check(_native.hip().lsk_hip_key_histogram(keys0.data_ptr(), keys0.shape[0], 30 - SPLIT_BITS,
+                                                   _hist_sample(keys0.shape[0]), hist.data_ptr(),
+                                                   K._stream(keys0)), "key_histogram")
+    elif keys0.numel():
+        sk = keys0[::_hist_sample(keys0.shape[0])]
+        hist += torch.bincount((sk.to(torch.int64) >> (30 - SPLIT_BITS)), minlength=nb).to(torch.int32)
+    comm.allreduce_(hist, "sum")
+    hist_h = hist.cpu()
+    splitters = _splitters(hist_h, max(1, int(hist_h.to(torch.int64).sum())), size)
+    info.timer.mark("partition")
+    recvs, rcs, perms, scs = [], [], [], []
+    for c, (s, e) in enumerate(spans):
+        pts_c = first if c == 0 else ready(c)
+        if c:
+            b = K.bounds(pts_c)
+            lo_hi = torch.cat([torch.minimum(lo_hi[0:3], b[0:3]), torch.maximum(lo_hi[3:6], b[3:6])])
+        keys_c = keys0 if c == 0 else K.morton(pts_c, box0, with_iota=False)[0]
+        perm_c, counts_c = _dest_and_perm(keys_c, splitters, size)
+        send_c = K.gather3(pts_c, perm_c)
+        sc = counts_c.cpu().tolist()
+        recv_c, rc = comm.alltoallv(send_c, sc)
+        recvs.append(recv_c)
+        rcs.append(rc)
+        perms.append(perm_c)
+        scs.append(sc)
+    info.timer.mark("alltoallv_points")
+    owned = torch.cat(recvs) if len(recvs) > 1 else recvs[0]
+    # exact global box (radius hint, local index keys)
+    v = torch.cat([lo_hi[0:3], -lo_hi[3:6]])
+    comm.allreduce_(v, "min")
+    box = torch.zeros(8, dtype=torch.float32, device=dev)
+    box[0:3] = v[0:3]
+    box[3:6] = -v[3:6]
+    box = K.box_finalize(box)
+    # return plan: owned rows are chunk-major, rank-minor; the return sends each rank its
+    # rows chunk by chunk, and the origin maps them back through the chunk permutations
+    ret_parts, ret_counts = [[] for _ in range(size)], [0] * size
+    orig_parts, back_counts = [[] for _ in range(size)], [0] * size
+    base = 0
+    for c, (s, e) in enumerate(spans):
+        ro = _offsets(rcs[c])
+        so = _offsets(scs[c])
+        for j in range(size):
+            if rcs[c][j]:
+                ret_parts[j].append(torch.arange(base + ro[j], base + ro[j + 1], device=dev))
+                ret_counts[j] += rcs[c][j]
+            if scs[c][j]:
+                orig_parts[j].append(perms[c][so[j]:so[j + 1]].to(torch.int64) + s)
+                back_counts[j] += scs[c][j]
+        base += ro[-1]
+    empty = torch.zeros(0, dtype=torch.int64, device=dev)
+    ret_index = torch.cat([t for parts in ret_parts for t in parts] or [empty])
+    origin_index = torch.cat([t for parts in orig_parts for t in parts] or [empty])
+    info.counts["sent_points"] = sum(sum(sc) - sc[comm.rank] for sc in scs)
+    info.counts["owned_points"] = int(owned.shape[0])
+    info.counts["stream_chunks"] = len(spans)
+    return Redist(owned, ret_index, ret_counts, origin_index, back_counts, box)
+
+
+def _offsets(counts):
+    o = [0]
+    for x in counts:
+        o.append(o[-1] + int(x))
+    return o
+
+
 def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
                 hint2: float | torch.Tensor,
                 info: RunInfo, final_out: torch.Tensor | None = None) -> torch.Tensor:
@@ -301,15 +429,21 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
 
 
 
+FORCE_STREAM = False  # tests: streamed redistribution also for device-resident input
+
+
 def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
                   n_total: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """k-th-NN distance of every local point (input order) for a globally unordered set
     block-partitioned over ranks (reference unorderedData variant).
 
+    `points` may live in (pinned) host memory: on several ranks the redistribution then
+    streams them to the device in chunks overlapped with the exchange
+    (redistribute_stream); on one rank they are copied first.
     `out` (optional, float32 [n_local]): where the distances go. On one rank the k-NN
     kernel writes them there directly — a pinned host tensor receives them straight over
     PCIe while the kernel runs (no device-to-host copy afterwards)."""
-    info = info or RunInfo(PhaseTimer(False, points.device))
+    info = info or RunInfo(PhaseTimer(False, comm.device))
     info.timer.start()
     points = points.contiguous()
     n_local = points.shape[0]
@@ -317,10 +451,14 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
         t = torch.tensor([n_local], dtype=torch.int64, device=comm.device)
         comm.allreduce_(t, "sum")
         n_total = int(t.item())
-    box = global_box(points, comm)
-    hint2 = E.radius_hint(box, n_total, cfg.k)
-    info.timer.mark("bounds")
+    streamed = comm.distributed and (points.device != comm.device or FORCE_STREAM)
+    if not streamed and points.device != comm.device:
+        points = points.to(comm.device, non_blocking=True)
+    dev = comm.device
     if not comm.distributed:
+        box = global_box(points, comm)
+        hint2 = E.radius_hint(box, n_total, cfg.k)
+        info.timer.mark("bounds")
         info.counts["owned_points"] = n_local
         index = E.build_index(points, box)
         info.timer.mark("build")
@@ -329,19 +467,32 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
         E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
         info.timer.mark("knn_local")
         return out
-    owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
+    if streamed:
+        R = redistribute_stream(points, comm, info)
+        box, owned = R.box, R.owned
+        hint2 = E.radius_hint(box, n_total, cfg.k)
+    else:
+        box = global_box(points, comm)
+        hint2 = E.radius_hint(box, n_total, cfg.k)
+        info.timer.mark("bounds")
+        owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
     index = E.build_index(owned, box)
     info.timer.mark("build")
     # final distances in received-row order straight from the kernels (fused scatter);
     # the sorted d2 feeds the halo radii and the re-query bounds
-    dist_owned = torch.empty(index.n, dtype=torch.float32, device=points.device)
+    dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None,
                  final_out=dist_owned, keep_d2=True)
     info.timer.mark("knn_local")
     halo_refine(index, d2, comm, cfg, hint2, info, final_out=dist_owned)
-    back, _ = comm.alltoallv(dist_owned, recv_counts)
-    res = torch.empty(n_local, dtype=torch.float32, device=points.device)
-    K.scatter1(back, send_perm, res, finalize=False)
+    res = torch.empty(n_local, dtype=torch.float32, device=dev)
+    if streamed:
+        # counts of the return are known from the send side: no count exchange
+        back, _ = comm.alltoallv(dist_owned[R.ret_index], R.ret_counts, recv_counts=R.back_counts)
+        K.scatter1(back, R.origin_index.to(torch.int32), res, finalize=False)
+    else:
+        back, _ = comm.alltoallv(dist_owned, recv_counts, recv_counts=send_counts)
+        K.scatter1(back, send_perm, res, finalize=False)
     info.timer.mark("return")
     if out is not None:
         out.copy_(res, non_blocking=True)

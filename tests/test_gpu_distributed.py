@@ -127,3 +127,25 @@ def test_unordered_multirank_gpu_sub_cell_core(size):
 
     out = torch.cat(run_loopback(size, fn, DEV))
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("size", [2, 4])
+def test_unordered_streamed_from_pinned_host(size, monkeypatch):
+    """Host-resident (pinned) input: the redistribution streams it to the device in chunks
+    on a copy stream, overlapped with the exchange; bit-identical to one rank."""
+    monkeypatch.setattr(PL, "STREAM_CHUNK", 40_000)
+    p = uniform(300_000, seed=21)
+    k = 100
+    ref = single(p, k)
+
+    def fn(comm):
+        b, e = block(p.shape[0], comm.rank, comm.size)
+        host = torch.empty((e - b, 3), dtype=torch.float32, pin_memory=True)
+        host.copy_(p[b:e])
+        info = PL.RunInfo(PL.PhaseTimer(False, DEV))
+        out = PL.unordered_knn(host, comm, E.KnnConfig(k=k), info)
+        return out.cpu(), info
+
+    res = run_loopback(size, fn, DEV)
+    assert torch.equal(torch.cat([r[0] for r in res]), ref)
+    assert all(r[1].counts["stream_chunks"] >= 2 for r in res)

@@ -236,3 +236,41 @@ def test_prepartitioned_skewed_files_rebalance(balance):
     else:
         assert all(i.counts.get("rebalanced") == 1 for i in infos)
         assert max(owned) < 1.1 * 16000 / size, owned
+
+
+@pytest.mark.parametrize("size", [1, 2, 3, 5])
+def test_unordered_streamed_redistribution(size, monkeypatch):
+    """Chunked (streamed) redistribution: ownership from the first chunks, return through
+    the chunk permutations; results equal the oracle in input order."""
+    monkeypatch.setattr(PL, "FORCE_STREAM", True)
+    monkeypatch.setattr(PL, "STREAM_CHUNK", 700)
+    p = clustered(7000, seed=size + 20)
+    k = 9
+    cfg = E.KnnConfig(k=k, publish_levels=4)
+    infos = [PL.RunInfo(PL.PhaseTimer(False, torch.device("cpu"))) for _ in range(size)]
+
+    def fn(comm):
+        b, e = block(p.shape[0], comm.rank, comm.size)
+        return PL.unordered_knn(p[b:e], comm, cfg, infos[comm.rank])
+
+    out = torch.cat(run_loopback(size, fn))
+    assert torch.equal(out, oracle(p, k))
+    if size > 1:
+        assert all(i.counts["stream_chunks"] >= 2 for i in infos)
+        assert sum(i.counts["owned_points"] for i in infos) == 7000
+
+
+def test_streamed_redistribution_unrepresentative_first_chunk(monkeypatch):
+    """Input sorted along x: the first chunk's cube misses most points (clamped keys) —
+    only the balance suffers, the result stays exact."""
+    monkeypatch.setattr(PL, "FORCE_STREAM", True)
+    monkeypatch.setattr(PL, "STREAM_CHUNK", 500)
+    p = uniform(4000, seed=3)
+    p = p[torch.argsort(p[:, 0])].contiguous()
+    cfg = E.KnnConfig(k=6, publish_levels=4)
+
+    def fn(comm):
+        b, e = block(p.shape[0], comm.rank, comm.size)
+        return PL.unordered_knn(p[b:e], comm, cfg)
+
+    assert torch.equal(torch.cat(run_loopback(3, fn)), oracle(p, 6))
