@@ -85,6 +85,9 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_BEST_FIRST
 #define LSK_BEST_FIRST 2
 #endif
+#ifndef LSK_ENTRY_PREFETCH
+#define LSK_ENTRY_PREFETCH 0
+#endif
 // walk/process alternation: the walk fills the row queues until every row has this
 // many entries pending (then one lockstep drain)
 #ifndef LSK_FILL_MIN
@@ -446,6 +449,11 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
   uint32_t cnt = load_quarter<NT>(W, row_entry(W, W.rhead), px, py, pz);
   // (two steps of prefetch: 0.155 vs 0.152 s at 6 waves/SIMD with 10 spilled VGPRs,
   // 0.166 s at 5 waves/SIMD — occupancy, not the candidate-load distance, is what counts)
+#if LSK_ENTRY_PREFETCH
+  // the queue entry of the next step is read from LDS one step early, so the candidate
+  // load address does not wait on an LDS round trip
+  uint32_t e_next = row_entry(W, W.rhead + (W.rhead < W.rlen ? 1u : 0u));
+#endif
   const float inf = __builtin_inff();
   for (uint32_t st = 0; st < n; st++) {
     const uint32_t ccnt = cnt;
@@ -453,7 +461,12 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     const bool live = (uint32_t)(W.lane & 15) < ccnt;
     const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
     W.rhead += W.rhead < W.rlen ? 1u : 0u;
+#if LSK_ENTRY_PREFETCH
+    cnt = load_quarter<NT>(W, e_next, px, py, pz);
+    e_next = row_entry(W, W.rhead + (W.rhead < W.rlen ? 1u : 0u));
+#else
     cnt = load_quarter<NT>(W, row_entry(W, W.rhead), px, py, pz);
+#endif
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
 #ifdef LSK_PROFILE
