@@ -17,7 +17,9 @@
 //     clipped at the -r cutoff.
 //  2. Radix select on the float bits of d² in [lo, hi): every pass walks the bucket
 //     trees (DFS, 8-ary expansion tested by 8 lanes, stack in LDS), prunes boxes whose
-//     distance is >= hi, and counts the values of each 64-point bucket (one point per
+//     distance is >= hi and boxes whose farthest corner is closer than lo (their values
+//     were counted by an earlier pass: a thin shell through a dense far cluster visits
+//     only the buckets it cuts), and counts the values of each 64-point bucket (one point per
 //     lane) into 256 32-bit LDS bins. The bin holding the k-th value becomes the next
 //     [lo, hi); a range of width 1 is the answer. <= 4 counting passes (8 bits each).
 // Same canonical dist² (common.h) as the oracle and the production kernel: bit-identical.
@@ -74,6 +76,15 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
     if ((uint32_t)lane < nc) {
       const float4 lo4 = nodes[2 * child], hi4 = nodes[2 * child + 1];
       need = lsk::box_dist2(q, {lo4.x, lo4.y, lo4.z}, {hi4.x, hi4.y, hi4.z}) < lim;
+      if (need && lo > 0u) {
+        // shell test: a box whose farthest corner is closer than bitsf(lo) holds only
+        // values below lo, already counted by the previous passes (per-axis float
+        // differences, squares and fma are monotone: no point inside is farther)
+        const float fx = fmaxf(fabsf(lo4.x - qx), fabsf(hi4.x - qx));
+        const float fy = fmaxf(fabsf(lo4.y - qy), fabsf(hi4.y - qy));
+        const float fz = fmaxf(fabsf(lo4.z - qz), fabsf(hi4.z - qz));
+        need = fbits(lsk::dist2(fx, fy, fz)) >= lo;
+      }
     }
     const uint64_t m = __ballot(need);
     if (need) {

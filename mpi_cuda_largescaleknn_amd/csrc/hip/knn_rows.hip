@@ -85,6 +85,11 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #ifndef LSK_BEST_FIRST
 #define LSK_BEST_FIRST 2
 #endif
+// a pass aborts and restarts with finer bins as soon as the bin holding some lane's k-th
+// value has more than this many times k entries (0 = off)
+#ifndef LSK_CROWD_ABORT
+#define LSK_CROWD_ABORT 64
+#endif
 #ifndef LSK_ENTRY_PREFETCH
 #define LSK_ENTRY_PREFETCH 0
 #endif
@@ -203,9 +208,39 @@ __device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *poo
   return s.bin_hi > 0 ? hist_read(pool, (uint32_t)s.bin_hi - 1u, lane) : s.c_hi;
 }
 
-__device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
+// A crowded k-th bin can be narrowed when shift > 0 (finer bins), or — bin 0 with an
+// unknown count below lo_b, the k-th may lie below the range — by one underflow restart.
+// Every restart lowers the shift or spends the one underflow: a lane restarts a bounded
+// number of times.
+__device__ __forceinline__ bool crowd_refinable(const Lane &s) {
+  return s.bin_hi >= 2 ? s.shift > 0u
+                       : (s.bin_hi == 1 && (s.shift > 0u || (s.c_base == kUnknown && s.nudf == 0)));
+}
+
+// Underflow restart: the k-th lies below lo_b (or bin 0 is too coarse to say). First time
+// the 5 octaves below the top; again (or a crowded bin 0: the values may lie any number
+// of octaves below, e.g. a dense cluster next to a far-off estimate): everything below in
+// kBins coarse bins.
+__device__ __forceinline__ void underflow_restart(Lane &s, bool coarse) {
+  const uint32_t topb = s.hi_b;  // = lo_b + 2^shift, or the clipped top
+  if (!coarse && s.nudf == 0 && topb > ((uint32_t)kBins << kShift0)) {
+    set_range(s, topb - ((uint32_t)kBins << kShift0), kShift0, topb, kUnknown);
+  } else {
+    uint32_t sh = 0;
+    while (((uint64_t)kBins << sh) < (uint64_t)topb) sh++;
+    set_range(s, 0u, sh, topb, 0u);
+  }
+  s.nudf++;
+}
+
+// Returns true when the bin now holding the k-th seen value is CROWDED (more than
+// kCrowd values, refinable: shift > 0, not the saturating bin 0): a dense cluster seen
+// from outside puts millions of candidates into one 1/8-octave bin, and the walk would
+// visit all of them (and overflow the 16-bit bin) before the pass could narrow the range.
+__device__ __forceinline__ bool hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
+  uint32_t top = 0;
   while (s.bin_hi > 0) {
-    const uint32_t top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
+    top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
     if (s.c_hi - top < k) break;
     s.c_hi -= top;
     s.bin_hi--;
@@ -216,6 +251,11 @@ __device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int l
   // box and candidate is culled), so k + duplicates of a point cost k candidates, not all
   // of them (and bin 0's 16-bit counter cannot overflow)
   if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
+#if LSK_CROWD_ABORT
+  return top > (uint32_t)LSK_CROWD_ABORT * k && crowd_refinable(s);
+#else
+  return false;
+#endif
 }
 
 // DPP row_newbcast:J — lane J of each 16-lane row to the whole row (folded into the
@@ -303,7 +343,7 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
 // The 16 candidates of this lane's row quarter (lane i of the row holds candidate i).
 template <int MODE>
 __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz, uint32_t cnt,
-                                          uint32_t *pool, int lane, uint32_t k) {
+                                          uint32_t *pool, int lane, uint32_t k, bool &crowd) {
   bool lane_in;
 #if LSK_CAND_GROUP == 4
   // groups of 4 candidates: 4 fewer live VGPRs in the hot loop than groups of 8
@@ -343,7 +383,7 @@ __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz,
     lane_in = update8<MODE, 8>(s, u, pool, lane) || lane_in;
   }
 #endif
-  if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) hist_shrink(s, pool, lane, k);
+  if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) crowd = __ballot(hist_shrink(s, pool, lane, k)) != 0 || crowd;
   return lane_in;
 }
 
@@ -371,6 +411,7 @@ struct WaveCtx {
   // 4 row bits per quarter) held by lane n % 64 of word n / 64 of two private arrays
   uint32_t logn;
   bool logging, log_ok;
+  bool crowd;  // a lane's k-th bin got crowded: abort the pass (see hist_shrink)
 #if LSK_LOG_PRUNE
   // pass-1 "dead row-step" stream: bit h of row r (lane 16r + h/32, bit h%32) is set when
   // the row's h-th queue entry gave no lane of the row a value below its bound; after
@@ -472,7 +513,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
 #ifdef LSK_PROFILE
     s.pband = false;
 #endif
-    const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k);
+    const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k, W.crowd);
 #ifdef LSK_PROFILE
     if (MODE == MODE_HIST) {
       const uint32_t re = row_bits(__ballot(ccnt > 0u)), ri = row_bits(__ballot(lin));
@@ -495,6 +536,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     (void)lin;
     (void)hcur;
 #endif
+    if (MODE == MODE_HIST && W.crowd) break;  // crowded bin: the pass restarts narrower
   }
   W.hd0 = min(W.hd0 + n, W.len0);
   W.hd1 = min(W.hd1 + n, W.len1);
@@ -1069,6 +1111,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     LSK_PT(tp0);
     process_steps<MODE, NT>(s, W, A, nsteps);
     LSK_PADD(W.prof[MODE], tp0);
+    if (MODE == MODE_HIST && W.crowd) break;  // aborted pass (the caller restarts it)
   }
 }
 
@@ -1183,6 +1226,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 #endif
   W.logn = 0;
   W.logging = W.log_ok = false;
+  W.crowd = false;
   W.p0 = A.tree[0].pts;
   W.p1 = A.ntrees > 1 ? A.tree[1].pts : A.tree[0].pts;
   W.n0 = A.ntrees > 0 ? (uint32_t)A.tree[0].n : 0u;
@@ -1338,6 +1382,35 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       else
         traverse<MODE_HIST, false, NT>(s, W, A);
       LSK_PADD(W.prof[2], tt0);
+      if (W.crowd) {
+        // aborted pass: counts are partial, but a shrunk top is still a valid bound (at
+        // least k values lie below it). Crowded lanes restart on their crowded bin in
+        // kBins finer bins (a k-th below it comes back through the underflow path), the
+        // others restart on their current range. The log is incomplete from here on.
+        W.crowd = false;
+        W.log_ok = false;
+        W.logging = false;
+        first = false;
+        if (s.state == ST_HIST) {
+          const uint32_t top = top_count(s, W.L->pool, lane);
+          if (s.c_hi >= k && top > (uint32_t)LSK_CROWD_ABORT * k && crowd_refinable(s)) {
+            qs |= QS_REFINE;
+            const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;
+            if (s.bin_hi >= 2) {
+              const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
+              set_range(s, bl, sh, s.hi_b, kUnknown);
+            } else if (s.c_base == kUnknown && s.nudf == 0) {
+              qs |= QS_UNDERFLOW;
+              underflow_restart(s, true);
+            } else {
+              set_range(s, s.lo_b, sh, s.hi_b, s.c_base);
+            }
+          } else {
+            set_range(s, s.lo_b, s.shift, s.hi_b > s.lo_b ? s.hi_b : s.cut_lim, s.c_base);
+          }
+        }
+        continue;
+      }
 #if LSK_LOG_PRUNE
       if (W.logging && W.log_ok) log_prune(W);
 #endif
@@ -1372,15 +1445,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
           // too large. First time: the 8 octaves below. Again: everything below, in 64
           // coarse bins (then refined) — also how a k-th distance of 0 is reached.
           qs |= QS_UNDERFLOW;
-          const uint32_t topb = s.hi_b;  // = lo_b + 2^shift, or the clipped top
-          if (s.nudf == 0 && topb > ((uint32_t)kBins << kShift0)) {
-            set_range(s, topb - ((uint32_t)kBins << kShift0), kShift0, topb, kUnknown);
-          } else {
-            uint32_t sh = 0;
-            while (((uint64_t)kBins << sh) < (uint64_t)topb) sh++;
-            set_range(s, 0u, sh, topb, 0u);
-          }
-          s.nudf++;
+          underflow_restart(s, false);
         } else {
           // band = bin bin_hi-1; bin 0 loses its saturated part (c_base values < lo_b)
           const uint32_t below = s.bin_hi == 1 ? s.c_base : s.c_hi - top;

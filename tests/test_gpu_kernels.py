@@ -281,8 +281,9 @@ def test_knn_two_bases_70000_copies(k):
 
 def test_knn_mixed_scale_exact():
     """Half the points uniform in a 1000-cube, half in a 0.001-cube at its centre: sparse
-    queries near the core see ~1e6 nearly equidistant candidates (16-bit bins overflow).
-    Every output finite and bit-identical to the oracle (failed queries -> backstop)."""
+    queries near the core see ~1e6 nearly equidistant candidates. Every output finite and
+    bit-identical to the oracle; crowded-bin pass restarts keep the 16-bit bins from
+    overflowing, so almost no query reaches the exact backstop (before them ~1 %)."""
     from datasets import mixed_scale
     p = mixed_scale(2_000_000, seed=3)
     stats = E.KnnStats()
@@ -291,6 +292,7 @@ def test_knn_mixed_scale_exact():
     assert bool(torch.isfinite(got).all()), stats.counters
     bad = int((got != ref).sum())
     assert bad == 0, f"{bad} mismatches; {stats.counters}"
+    assert stats.counters.get("failed_lanes", 0) <= p.shape[0] // 5000, stats.counters
 
 
 @pytest.mark.parametrize("mod", [1, 7, 1000])
