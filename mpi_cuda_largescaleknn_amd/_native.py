@@ -164,6 +164,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_refalgo_extract": ([vp, i64, i32, vp, vp], i32),
         "lsk_hip_count_below": ([vp, i64, vp, vp, i32, vp, vp], i32),
         "lsk_hip_segment_bounds": ([vp, vp, i64, i64, vp, vp, vp], i32),
+        "lsk_hip_screen_ab": ([vp, i64, vp, i32, i32, vp, vp, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

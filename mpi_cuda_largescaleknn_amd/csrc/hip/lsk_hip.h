@@ -182,6 +182,12 @@ int lsk_hip_refalgo_extract(const unsigned long long *heaps, int64_t nq, int k, 
 int lsk_hip_count_below(const float *pts, int64_t n, const float *q, const float *thr, int nq,
                         unsigned long long *counts, void *stream);
 
+// ---- MFMA vs VALU screening A/B (screen_ab.hip) -------------------------------------------
+// n curve-ordered points (n % 64 == 0) are also the queries; out[q] = kept pairs per lane;
+// mode 0 VALU canonical, 1 MFMA screen, 2 MFMA screen + viol += pairs wrongly dropped.
+int lsk_hip_screen_ab(const float *pts, int64_t n, const float *thr, int steps, int mode, uint32_t *out,
+                      uint32_t *viol, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -344,3 +344,49 @@ def test_segment_bounds_kernel_matches_torch():
     rlo = torch.full((lens.shape[0], 3), float("inf")).scatter_reduce(0, idx3, p, "amin")
     rhi = torch.full((lens.shape[0], 3), -float("inf")).scatter_reduce(0, idx3, p, "amax")
     assert torch.equal(lo.cpu(), rlo) and torch.equal(hi.cpu(), rhi)
+
+
+@pytest.mark.parametrize("dist", ["uniform", "clustered", "mixed_scale"])
+def test_mfma_screen_is_conservative(dist):
+    """screen_ab.hip: the MFMA 16x16x4 screen (row-centred |q'|^2 - 2q'.p' + |p'|^2 with an
+    f32 error margin) never drops a (query, candidate) pair whose canonical d^2 is below
+    the threshold, keeps few extra pairs, and the VALU form counts exactly
+    the canonical pairs. mixed_scale puts the points near 500 (large coordinates, tiny
+    distances: the centring is what keeps the margin small)."""
+    from mpi_cuda_largescaleknn_amd import _native
+
+    n, steps = 1 << 16, 24
+    p = GENERATORS[dist](n).to(DEV)
+    idx = E.build_index(p)
+    sp = idx.pts[:n].contiguous()
+    thr = (E.knn_distances(sp, 16).double() ** 2 * 1.5).float().contiguous()
+    lib = _native.hip()
+    outs = []
+    viol = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for mode in (0, 1, 2):
+        out = torch.zeros(n, dtype=torch.int32, device=DEV)
+        K.check(lib.lsk_hip_screen_ab(sp.data_ptr(), n, thr.data_ptr(), steps, mode, out.data_ptr(),
+                                      viol.data_ptr(), K._stream(sp)), "screen_ab")
+        outs.append(int(out.long().sum()))
+    torch.cuda.synchronize()
+    assert int(viol.item()) == 0
+    assert outs[1] == outs[2]
+    # the f32 margin is relative (~4e-6): on the mixed_scale core lattice many pairs sit at
+    # exactly the same d^2 just above the threshold, elsewhere it keeps < 0.5 % extra
+    slack = 1.10 if dist == "mixed_scale" else 1.005
+    assert outs[0] > 0 and outs[0] <= outs[1] <= outs[0] * slack + 64, outs
+    # VALU count vs a float64 recount of the same pairs (ties at the threshold aside)
+    q = sp.double().cpu()
+    t = thr.double().cpu()
+    nq4 = n // 16
+    lane = torch.arange(n)
+    g, r = lane // 64, (lane % 64) // 16
+    tot = 0
+    for s in range(steps):
+        qid = 4 * (g + s - steps // 2) + r
+        qid = torch.where(qid < 0, qid & 3, qid)
+        qid = torch.where(qid >= nq4, nq4 - 4 + (qid & 3), qid)
+        cand = q[(16 * qid)[:, None] + torch.arange(16)[None, :]]
+        d2 = ((q[:, None, :] - cand) ** 2).sum(-1)
+        tot += int((d2 < t[:, None]).sum())
+    assert abs(tot - outs[0]) <= max(8, tot // 100000), (tot, outs[0])
