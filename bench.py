@@ -41,8 +41,10 @@ from mpi_cuda_largescaleknn_amd.utils import trace, verify  # noqa: E402
 
 HEADLINE_METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
 GEN_CHUNK = 1 << 24  # points per seeded generation chunk (global index -> seed)
-PHASES = ["bounds", "partition", "alltoallv_points", "build", "knn_local", "halo_publish",
-          "halo_filter", "halo_alltoallv", "halo_tree", "halo_requery", "return"]
+# "knn_local+halo_exchange": the overlapped form (pipelines.knn_with_halo) — the local k-NN
+# and the halo publish/filter/exchange on a side stream end at one mark
+PHASES = ["bounds", "partition", "alltoallv_points", "build", "knn_local", "knn_local+halo_exchange",
+          "halo_publish", "halo_filter", "halo_alltoallv", "halo_tree", "halo_requery", "return"]
 COUNTS = ["sent_points", "owned_points", "halo_sent", "halo_recv", "requery_groups"]
 
 
@@ -279,7 +281,9 @@ def instrumented_detail(comm, run_step, last_info) -> dict:
     return {
         "phase_ms_max_over_ranks": phases_max,
         "instrumented_step_ms_per_rank": [round(float(x) * 1e3, 3) for x in allv[:, np_]],
-        "knn_local_ms_per_rank": [round(float(x) * 1e3, 3) for x in allv[:, PHASES.index("knn_local")]],
+        "knn_local_ms_per_rank": [round(float(max(a, b)) * 1e3, 3) for a, b in
+                                  zip(allv[:, PHASES.index("knn_local")],
+                                      allv[:, PHASES.index("knn_local+halo_exchange")])],
         "halo_requery_ms_per_rank": [round(float(x) * 1e3, 3) for x in allv[:, PHASES.index("halo_requery")]],
         "redistributed_bytes": counts_sum["sent_points"] * 12,
         "halo_bytes": counts_sum["halo_sent"] * 12,

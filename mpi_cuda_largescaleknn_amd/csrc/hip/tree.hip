@@ -112,7 +112,58 @@ __global__ __launch_bounds__(256) void leaf_radius_kernel(const float *__restric
   if (lsk::lane_id() == 0) nodes[8 * (((int64_t)1 << depth) + leaf) + 3] = r;
 }
 
+// A-priori upper bound of every leaf's k-th squared radius, before any k-NN runs (the
+// overlapped halo exchange publishes it while the local k-NN is still running): the
+// W = ceil(k/64) + 1 consecutive buckets around the leaf hold >= k points (the query
+// itself included), so no query of the leaf has its k-th neighbour farther than the
+// farthest corner pair of the leaf box and the window's union box. Padded by 2^-16
+// relative (far above the rounding of the canonical d2 the kernels compare). n < k:
+// +inf (fewer than k local points: the local k-th is infinite).
+__global__ __launch_bounds__(256) void leaf_radius_ub_kernel(int64_t n, int k, float *__restrict__ nodes,
+                                                             int depth, int64_t nleaf_slots) {
+  const int64_t leaf = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (leaf >= nleaf_slots) return;
+  const int64_t nb = (n + lsk::kBucket - 1) / lsk::kBucket;
+  const int64_t slots = (int64_t)1 << depth;
+  const float4 *nd = (const float4 *)nodes;
+  float r = 0.f;
+  if (leaf < nb) {
+    if (n < (int64_t)k) {
+      r = __builtin_inff();
+    } else {
+      const int64_t W = min(nb, (int64_t)(k + lsk::kBucket - 1) / lsk::kBucket + 1);
+      int64_t st = leaf - (W - 1) / 2;
+      st = st < 0 ? 0 : (st > nb - W ? nb - W : st);
+      const float inf = __builtin_inff();
+      float wlx = inf, wly = inf, wlz = inf, whx = -inf, why = -inf, whz = -inf;
+      for (int64_t b = st; b < st + W; b++) {
+        const float4 lo = nd[2 * (slots + b)], hi = nd[2 * (slots + b) + 1];
+        wlx = fminf(wlx, lo.x); wly = fminf(wly, lo.y); wlz = fminf(wlz, lo.z);
+        whx = fmaxf(whx, hi.x); why = fmaxf(why, hi.y); whz = fmaxf(whz, hi.z);
+      }
+      const float4 lo = nd[2 * (slots + leaf)], hi = nd[2 * (slots + leaf) + 1];
+      const float ex = fmaxf(whx - lo.x, hi.x - wlx), ey = fmaxf(why - lo.y, hi.y - wly),
+                  ez = fmaxf(whz - lo.z, hi.z - wlz);
+      r = lsk::dist2(ex, ey, ez) * (1.f + 0x1p-16f);
+    }
+  }
+  nodes[8 * (slots + leaf) + 3] = r;
+}
+
 }  // namespace
+
+extern "C" int lsk_hip_tree_set_radii_ub(float *nodes, int64_t n, int k, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int depth = lsk_hip_tree_depth(n);
+  const int64_t slots = (int64_t)1 << depth;
+  leaf_radius_ub_kernel<<<lsk_blocks(slots, 256), 256, 0, s>>>(n, k, nodes, depth, slots);
+  LSK_CHECK_LAUNCH("tree_leaf_radius_ub");
+  for (int l = depth - 1; l >= 0; l--) {
+    levelup_kernel<<<lsk_blocks((int64_t)1 << l, 256), 256, 0, s>>>(nodes, l, 1);
+    LSK_CHECK_LAUNCH("tree_levelup_radius");
+  }
+  return 0;
+}
 
 extern "C" int lsk_hip_tree_depth(int64_t n) {
   int64_t nb = (n + lsk::kBucket - 1) / lsk::kBucket;

@@ -249,13 +249,17 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
           groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
           init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None,
-          keep_d2: bool = False) -> torch.Tensor:
+          keep_d2: bool = False, deferred: list | None = None) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
     `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order.
 
     With `final_out` the kernel also writes the final distances in input order
     (final_out[index.perm[q]], fused scatter); then the sorted d2 is only produced (and
-    returned) when `keep_d2` or `out` is given, else final_out is returned."""
+    returned) when `keep_d2` or `out` is given, else final_out is returned.
+
+    `deferred` (a list): the failure-word read (a host sync) is not done here but queued
+    on the list; `settle(deferred)` does it later — the launch stays asynchronous, so the
+    host can queue other work (the overlapped halo exchange) behind it."""
     n = index.n
     want_d2 = final_out is None or keep_d2 or out is not None
     if out is None and want_d2:
@@ -288,9 +292,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
               out_perm=index.perm if final_out is not None else None, out_final=final_out)
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl=KNN_IMPL, debug_fail_mod=DEBUG_FAIL_MOD, **kw)
-    if torch.cuda.is_current_stream_capturing():
-        CAPTURED_FAIL_WORDS.append(fw)
-    elif fw.count is not None:
+    def check():
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun
         # the whole query on the exact kernel
         nfail = fw.value()
@@ -298,9 +300,26 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
             K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", **kw)
         if stats is not None:
             stats.add_fallback(nfail)
-    if stats is not None:
-        stats.add(raw)
+            stats.add(raw)
+
+    if torch.cuda.is_current_stream_capturing():
+        CAPTURED_FAIL_WORDS.append(fw)
+        if stats is not None:
+            stats.add(raw)
+    elif fw.count is None:
+        if stats is not None:
+            stats.add(raw)
+    elif deferred is not None:
+        deferred.append(check)
+    else:
+        check()
     return out if want_d2 else final_out
+
+
+def settle(deferred: list) -> None:
+    """Run the failure checks `query(..., deferred=...)` queued (in launch order)."""
+    while deferred:
+        deferred.pop(0)()
 
 
 def verify_captured_failures(clear: bool = False) -> int:

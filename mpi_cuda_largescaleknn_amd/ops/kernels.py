@@ -335,6 +335,40 @@ def kth_cpu(points: torch.Tensor, queries: torch.Tensor, k: int, cut2: float, me
 
 
 # --------------------------------------------------------------------------- halo
+def tree_set_radii_ub(nodes: torch.Tensor, n: int, k: int) -> torch.Tensor:
+    """Per-node upper bound of the k-th squared radius before any query ran: the
+    ceil(k/64)+1 buckets around each leaf hold >= k points, so a leaf's k-th neighbour
+    lies within the farthest corner pair of its box and their union box (tree.hip
+    leaf_radius_ub_kernel; same arithmetic here)."""
+    if is_gpu(nodes):
+        check(_native.hip().lsk_hip_tree_set_radii_ub(_ptr(nodes), n, k, _stream(nodes)), "tree_set_radii_ub")
+        return nodes
+    depth = tree_depth(n)
+    slots = 1 << depth
+    nb = (n + BUCKET - 1) // BUCKET
+    r = torch.zeros(slots, dtype=torch.float32)
+    if nb and n < k:
+        r[:nb] = math.inf
+    elif nb:
+        w = min(nb, (k + BUCKET - 1) // BUCKET + 1)
+        leaf = torch.arange(nb)
+        st = (leaf - (w - 1) // 2).clamp(0, nb - w)
+        lo = nodes[slots:slots + nb, 0:3]
+        hi = nodes[slots:slots + nb, 4:7]
+        win = st[:, None] + torch.arange(w)[None, :]
+        wlo = lo[win].amin(dim=1)
+        whi = hi[win].amax(dim=1)
+        e = torch.maximum(whi - lo, hi - wlo)
+        d2 = torch.addcmul(torch.addcmul(e[:, 0] * e[:, 0], e[:, 1], e[:, 1]), e[:, 2], e[:, 2])
+        r[:nb] = d2 * (1.0 + 2.0 ** -16)
+    nodes[slots:, 3] = r
+    for level in range(depth - 1, -1, -1):
+        a = 1 << level
+        ch = nodes[2 * a: 4 * a].view(a, 2, 8)
+        nodes[a:2 * a, 3] = torch.maximum(ch[:, 0, 3], ch[:, 1, 3])
+    return nodes
+
+
 def halo_mask(pts: torch.Tensor, pub: torch.Tensor, pub_off: list[int], pub_depth: list[int], self_rank: int) -> torch.Tensor:
     """Per point bitmask of ranks whose published radius-inflated boxes contain it."""
     n = pts.shape[0]

@@ -130,7 +130,13 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         if backend == "nccl":
             if not use_gpu:
                 raise ValueError("LSKNN_DIST_BACKEND=nccl needs a GPU run")
-            dist.init_process_group("nccl", rank=rank, world_size=size, device_id=device, timeout=timeout)
+            # RCCL's internal streams at high priority: the halo exchange runs while the
+            # local k-NN grid fills every CU (pipelines.knn_with_halo), and a normal-priority
+            # collective kernel would only get CUs when that grid drains
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", rank=rank, world_size=size, device_id=device, timeout=timeout,
+                                    pg_options=opts)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
         comm: Comm = TorchComm(device, force=force_distributed)

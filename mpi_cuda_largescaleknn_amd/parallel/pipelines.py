@@ -24,6 +24,7 @@ The reference-faithful schedules (ring rotation, peer pulls) live in ``refalgo.p
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -314,30 +315,27 @@ def _offsets(counts):
     return o
 
 
-def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
-                hint2: float | torch.Tensor,
-                info: RunInfo, final_out: torch.Tensor | None = None) -> torch.Tensor:
-    """Exchange boundary candidates and re-query the affected query groups (exact).
-    `final_out` (input order of index.perm) already holds the local final distances; the
-    re-query updates it in place together with the sorted d2."""
+def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo,
+               marks: bool = True) -> torch.Tensor:
+    """Publish the top levels of `radii_nodes` (index's tree with per-node k-th squared
+    radius bounds in lo.w), filter and pack own points for every other rank, exchange:
+    returns the received halo points."""
     size, rank = comm.size, comm.rank
     n = index.n
     dev = index.device
     levels = cfg.publish_levels
-    # 1. publish top levels of the radius-annotated tree
-    K.tree_set_radii(index.nodes, n, d2)
     my_levels = min(levels, index.depth)
     rows = 2 << levels
     pub = torch.zeros((rows, 8), dtype=torch.float32, device=dev)
     pub[:, 0:3] = math.inf
     pub[:, 4:7] = -math.inf
-    take = min(rows, index.nodes.shape[0], 2 << my_levels)
-    pub[:take] = index.nodes[:take]
+    take = min(rows, radii_nodes.shape[0], 2 << my_levels)
+    pub[:take] = radii_nodes[:take]
     meta = torch.tensor([my_levels], dtype=torch.int32, device=dev)
     pub_all = comm.allgather(pub)                       # [P, rows, 8]
     depths = comm.allgather(meta).view(-1).cpu().tolist()
-    info.timer.mark("halo_publish")
-    # 2. filter and pack own points for every other rank
+    if marks:
+        info.timer.mark("halo_publish")
     pts = index.pts[:n]
     offs = [j * rows * 8 for j in range(size)]
     mask = K.halo_mask(pts, pub_all.reshape(-1), offs, depths, rank)
@@ -363,28 +361,39 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
             parts.append(pts[sel])
             send_counts.append(int(sel.sum()))
         send = torch.cat(parts) if parts else pts[:0]
-    info.timer.mark("halo_filter")
-    recv, recv_counts = comm.alltoallv(send, send_counts)
+    if marks:
+        info.timer.mark("halo_filter")
+    recv, _ = comm.alltoallv(send, send_counts)
     info.counts["halo_sent"] = int(sum(send_counts))
     info.counts["halo_recv"] = int(recv.shape[0])
-    info.timer.mark("halo_alltoallv")
+    if marks:
+        info.timer.mark("halo_alltoallv")
+    return recv
+
+
+def _halo_requery(index: E.LocalIndex, d2: torch.Tensor, recv: torch.Tensor, cfg: E.KnnConfig,
+                  hint2: float | torch.Tensor, info: RunInfo, final_out: torch.Tensor | None) -> torch.Tensor:
+    """Halo tree from the received points; re-query (against local + halo) every query
+    group a halo point can reach within its local k-th radius (index.nodes must carry the
+    final radii: tree_set_radii). Updates d2 / final_out in place."""
+    n = index.n
+    dev = index.device
     nh = recv.shape[0]
     if nh == 0 or n == 0:
         return d2
-    # 3. halo tree, flag affected groups, re-query them against local + halo
     hidx = E.build_index(recv)
-    if K.is_gpu(pts):
+    if K.is_gpu(index.pts):
         from .. import _native
         lib = _native.hip()
         ng = (n + 63) // 64
         flags = torch.zeros(ng, dtype=torch.int32, device=dev)
-        # halo points against the local radius-annotated tree (tree_set_radii above)
+        # halo points against the local radius-annotated tree
         K.check(lib.lsk_hip_flag_groups_inverse(hidx.pts.data_ptr(), nh, index.nodes.data_ptr(), index.depth,
-                                                ng, flags.data_ptr(), K._stream(pts)), "flag_groups")
+                                                ng, flags.data_ptr(), K._stream(index.pts)), "flag_groups")
         glist = torch.empty(ng, dtype=torch.int32, device=dev)
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         K.check(lib.lsk_hip_compact_flags(flags.data_ptr(), ng, glist.data_ptr(), cnt.data_ptr(),
-                                          K._stream(pts)), "compact_flags")
+                                          K._stream(index.pts)), "compact_flags")
         nflag = int(cnt.item())
         info.counts["requery_groups"] = nflag
         info.timer.mark("halo_tree")
@@ -398,6 +407,85 @@ def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnCon
         E.query(index, cfg, hint2, extra=hidx, out=d2, final_out=final_out)
     info.timer.mark("halo_requery")
     return d2
+
+
+def halo_refine(index: E.LocalIndex, d2: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
+                hint2: float | torch.Tensor,
+                info: RunInfo, final_out: torch.Tensor | None = None) -> torch.Tensor:
+    """Exchange boundary candidates and re-query the affected query groups (exact).
+    `final_out` (input order of index.perm) already holds the local final distances; the
+    re-query updates it in place together with the sorted d2."""
+    K.tree_set_radii(index.nodes, index.n, d2)
+    recv = _halo_send(index, index.nodes, comm, cfg, info)
+    return _halo_requery(index, d2, recv, cfg, hint2, info, final_out)
+
+
+# Overlapped halo exchange (SURVEY §7.5 H6; the reference rotates shards only after the
+# local query, unorderedDataVariant.cu:204). The halo filter needs per-node radius bounds;
+# instead of waiting for the local k-NN's radii, a copy of the tree gets a-priori upper
+# bounds from the bucket boxes (K.tree_set_radii_ub: the ceil(k/64)+1 buckets around a
+# leaf hold >= k points), and publish / filter / pack / alltoallv run on a side stream
+# while the local k-NN kernel runs on the compute stream. The halo is a superset of the
+# exact one (looser radii); the re-query flags groups with the final radii, so the result
+# is unchanged. Env LSKNN_OVERLAP_HALO=0 restores the sequential order.
+OVERLAP_HALO = os.environ.get("LSKNN_OVERLAP_HALO", "1") != "0"
+_SIDE_STREAMS: dict = {}
+
+
+def _overlap_streams(dev: torch.device):
+    """(compute, side) non-blocking streams of this thread (loopback ranks are threads).
+    The k-NN also leaves the default stream: any implicit default-stream synchronisation
+    on the side path (pageable copies) must not wait for the k-NN kernel. The side stream
+    has the high priority: once the k-NN grid fills every CU, a side kernel only starts
+    when the dispatcher prefers its queue as k-NN workgroups retire."""
+    import threading
+    key = (threading.get_ident(), dev.index)
+    st = _SIDE_STREAMS.get(key)
+    if st is None:
+        hi = torch.cuda.Stream.priority_range()[1]  # (low, high): high is the smaller number
+        st = _SIDE_STREAMS[key] = (torch.cuda.Stream(dev), torch.cuda.Stream(dev, priority=hi))
+    return st
+
+
+def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: float | torch.Tensor,
+                  info: RunInfo, final_out: torch.Tensor) -> torch.Tensor:
+    """Local k-NN of every owned query + halo exchange + re-query (distributed runs).
+    Returns the sorted d2; `final_out` receives the final distances (index.perm order)."""
+    stats = info.stats if cfg.collect_stats else None
+    gpu = K.is_gpu(index.pts)
+    if not OVERLAP_HALO or (gpu and torch.cuda.is_current_stream_capturing()):
+        d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
+        info.timer.mark("knn_local")
+        return halo_refine(index, d2, comm, cfg, hint2, info, final_out=final_out)
+    if not gpu:  # same data flow, no streams to overlap on
+        ub = K.tree_set_radii_ub(index.nodes.clone(), index.n, cfg.k)
+        recv = _halo_send(index, ub, comm, cfg, info, marks=False)
+        d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
+        info.timer.mark("knn_local+halo_exchange")
+        K.tree_set_radii(index.nodes, index.n, d2)
+        return _halo_requery(index, d2, recv, cfg, hint2, info, final_out)
+    dev = index.device
+    cur = torch.cuda.current_stream(dev)
+    comp, side = _overlap_streams(dev)
+    comp.wait_stream(cur)
+    side.wait_stream(cur)
+    pend: list = []
+    with torch.cuda.stream(comp):
+        d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True, deferred=pend)
+    with torch.cuda.stream(side):
+        ub = index.nodes.clone()
+        K.tree_set_radii_ub(ub, index.n, cfg.k)
+        recv = _halo_send(index, ub, comm, cfg, info, marks=False)
+    cur.wait_stream(comp)
+    cur.wait_stream(side)
+    recv.record_stream(cur)
+    d2.record_stream(cur)
+    final_out.record_stream(comp)
+    E.settle(pend)
+    info.counts["halo_overlap"] = 1
+    info.timer.mark("knn_local+halo_exchange")
+    K.tree_set_radii(index.nodes, index.n, d2)
+    return _halo_requery(index, d2, recv, cfg, hint2, info, final_out)
 
 
 # --------------------------------------------------------------------------- entrypoints
@@ -481,10 +569,7 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     # final distances in received-row order straight from the kernels (fused scatter);
     # the sorted d2 feeds the halo radii and the re-query bounds
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
-    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None,
-                 final_out=dist_owned, keep_d2=True)
-    info.timer.mark("knn_local")
-    halo_refine(index, d2, comm, cfg, hint2, info, final_out=dist_owned)
+    knn_with_halo(index, comm, cfg, hint2, info, dist_owned)
     res = torch.empty(n_local, dtype=torch.float32, device=dev)
     if streamed:
         # counts of the return are known from the send side: no count exchange
@@ -545,10 +630,7 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
         info.timer.mark("knn_local")
         return out
     res = torch.empty(n_local, dtype=torch.float32, device=points.device)
-    d2 = E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None,
-                 final_out=res, keep_d2=True)
-    info.timer.mark("knn_local")
-    halo_refine(index, d2, comm, cfg, hint2, info, final_out=res)
+    knn_with_halo(index, comm, cfg, hint2, info, res)
     info.timer.mark("return")
     if out is not None:
         out.copy_(res, non_blocking=True)

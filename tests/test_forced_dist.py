@@ -49,7 +49,7 @@ def test_forced_one_rank_gloo_equals_single(tmp_path):
     for name in ("unordered", "prepartitioned", "ring", "peer"):
         assert torch.equal(res[name], res[name + "_single"]), name
     assert "alltoallv_points" in res["unordered_phases"]
-    assert "halo_alltoallv" in res["prepartitioned_phases"]
+    assert "knn_local+halo_exchange" in res["prepartitioned_phases"]  # overlapped halo (default)
 
 
 def _chunk_worker(rank, size, port, out_dir):

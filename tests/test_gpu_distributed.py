@@ -149,3 +149,29 @@ def test_unordered_streamed_from_pinned_host(size, monkeypatch):
     res = run_loopback(size, fn, DEV)
     assert torch.equal(torch.cat([r[0] for r in res]), ref)
     assert all(r[1].counts["stream_chunks"] >= 2 for r in res)
+
+
+@pytest.mark.parametrize("k", [16, 100])
+def test_overlapped_halo_gpu_equals_sequential(k, monkeypatch):
+    """The side-stream halo exchange (a-priori radius bounds, publish/filter/pack/exchange
+    while the local k-NN kernel runs) gives the sequential form's bits; its halo is a
+    superset of the sequential one; the overlapped path really ran."""
+    p = clustered(300_000, seed=k)
+    ref = single(p, k)
+    cfg = E.KnnConfig(k=k)
+    res = {}
+    for mode in (False, True):
+        monkeypatch.setattr(PL, "OVERLAP_HALO", mode)
+
+        def fn(comm):
+            b, e = block(p.shape[0], comm.rank, comm.size)
+            info = PL.RunInfo(PL.PhaseTimer(False, DEV))
+            out = PL.unordered_knn(p[b:e].to(DEV), comm, cfg, info)
+            return out.cpu(), info
+
+        r = run_loopback(4, fn, DEV)
+        res[mode] = (torch.cat([x[0] for x in r]), sum(x[1].counts["halo_recv"] for x in r),
+                     [x[1].counts.get("halo_overlap", 0) for x in r])
+    assert torch.equal(res[True][0], ref) and torch.equal(res[False][0], ref)
+    assert res[True][1] >= res[False][1]
+    assert res[True][2] == [1, 1, 1, 1] and res[False][2] == [0, 0, 0, 0]

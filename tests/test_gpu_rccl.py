@@ -36,7 +36,9 @@ def _worker(rank, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True  # as parallel/launch.py
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, pg_options=opts)
     comm = TorchComm(dev, force=True)
     assert comm.backend == "nccl" and comm.distributed and not comm.staged
     one = SingleComm(dev)

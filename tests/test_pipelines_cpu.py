@@ -274,3 +274,43 @@ def test_streamed_redistribution_unrepresentative_first_chunk(monkeypatch):
         return PL.unordered_knn(p[b:e], comm, cfg)
 
     assert torch.equal(torch.cat(run_loopback(3, fn)), oracle(p, 6))
+
+
+@pytest.mark.parametrize("k", [5, 100, 300])
+def test_overlapped_halo_superset_and_exact(k, monkeypatch):
+    """knn_with_halo's overlapped form publishes a-priori radius bounds (tree_set_radii_ub,
+    before any query ran): its halo is a superset of the sequential form's (exact radii),
+    the re-query flags from the final radii, and the results are identical (and exact).
+    k = 300 > 64: the bound window spans several buckets; 4 ranks, clustered data."""
+    p = clustered(8000, seed=k)
+    cfg = E.KnnConfig(k=k, publish_levels=4)
+    res = {}
+    for mode in (False, True):
+        monkeypatch.setattr(PL, "OVERLAP_HALO", mode)
+        infos = [PL.RunInfo(PL.PhaseTimer(False, torch.device("cpu"))) for _ in range(4)]
+
+        def fn(comm):
+            b, e = block(p.shape[0], comm.rank, comm.size)
+            return PL.unordered_knn(p[b:e], comm, cfg, infos[comm.rank])
+
+        res[mode] = (torch.cat(run_loopback(4, fn)), sum(i.counts.get("halo_recv", 0) for i in infos))
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][0], oracle(p, k))
+    assert res[True][1] >= res[False][1] > 0
+
+
+def test_radius_upper_bound_covers_kth():
+    """Every leaf's a-priori bound >= the largest k-th squared distance of its queries."""
+    for n, k in ((5000, 1), (5000, 64), (5000, 65), (3000, 200), (100, 100), (50, 100)):
+        p = uniform(n, seed=n + k)
+        idx = E.build_index(p)
+        nodes = K.tree_set_radii_ub(idx.nodes.clone(), idx.n, k)
+        d2 = K.kth_cpu(idx.pts[:n], idx.pts[:n], k, math.inf)
+        slots = 1 << idx.depth
+        nb = (n + 63) // 64
+        leaf_max = torch.zeros(slots * 64)
+        leaf_max[:n] = d2
+        leaf_max = leaf_max.view(slots, 64).amax(dim=1)
+        ub = nodes[slots:slots + nb, 3]
+        assert bool((ub >= leaf_max[:nb]).all()), (n, k)
+        assert float(nodes[1, 3]) >= float(d2.max())
