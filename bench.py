@@ -253,6 +253,8 @@ def main():
                                 f"spatial-redistribute+halo x{world}" if args.variant == "unordered"
                                 else f"halo x{world}"),
                 "k": args.k,
+                "comm": (getattr(getattr(comm, "inner", comm), "backend", "single")
+                         if comm.distributed else "single"),
                 "hip_graph": graph is not None,
                 "heavy_cells_unrefined": heavy_unrefined,
                 "all_finite": finite,

@@ -4,6 +4,7 @@
   built with g++.
 * ``lib/liblsknn_hip.so``   — hand-written gfx950 HIP kernels, built with
   ``hipcc --offload-arch=gfx950`` (cross-compiles without a GPU).
+* ``lib/liblsknn_comm.so``  — native RCCL communicator (host code, RCCL dlopen'ed).
 
 Both are rebuilt only when a source or header is newer than the library. The
 libraries are git-ignored but travel to the GPU box with the working tree.
@@ -107,7 +108,26 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     return HIP_LIB
 
 
+COMM_LIB = os.path.join(LIB_DIR, "liblsknn_comm.so")
+
+
+def build_comm(force: bool = False, verbose: bool = False) -> str:
+    """Native RCCL communicator (csrc/comm): host C++ against the HIP runtime and the
+    RCCL headers; RCCL itself is dlopen'ed at run time (no link-time dependency)."""
+    srcs = _sources("comm", "cpp")
+    if force or _stale(COMM_LIB, srcs + _headers()):
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = COMM_LIB + ".tmp"
+        cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", tmp, *srcs, "-ldl"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        _run(cmd)
+        os.replace(tmp, COMM_LIB)
+    return COMM_LIB
+
+
 def build_all(force: bool = False, verbose: bool = False) -> tuple[str, str]:
+    build_comm(force, verbose)
     return build_host(force, verbose), build_hip(force, verbose)
 
 
@@ -115,3 +135,4 @@ if __name__ == "__main__":
     force = "--force" in sys.argv
     for p in build_all(force=force, verbose=True):
         print(p)
+    print(COMM_LIB)

@@ -213,6 +213,31 @@ def hip() -> C.CDLL:
     return _hip_lib
 
 
+_comm_lib = None
+
+
+def comm() -> C.CDLL:
+    """The native RCCL communicator library (csrc/comm/rccl_comm.cpp)."""
+    global _comm_lib
+    if _comm_lib is None:
+        with _lock:
+            if _comm_lib is None:
+                path = _build.build_comm()
+                lib = C.CDLL(path)
+                lib.lsk_comm_last_error.restype = C.c_char_p
+                lib.lsk_comm_load.argtypes = [C.c_char_p]
+                lib.lsk_comm_version.argtypes = [C.POINTER(C.c_int)]
+                lib.lsk_comm_unique_id.argtypes = [C.c_char_p, i32]
+                lib.lsk_comm_init.argtypes = [C.c_char_p, i32, i32, i32, C.POINTER(vp)]
+                lib.lsk_comm_destroy.argtypes = [vp, i32]
+                lib.lsk_comm_allreduce.argtypes = [vp, vp, i64, i32, i32, vp]
+                lib.lsk_comm_allgather.argtypes = [vp, vp, vp, i64, vp]
+                lib.lsk_comm_alltoallv.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, i64, i32, vp]
+                lib.lsk_comm_sendrecv.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, i64, vp]
+                _comm_lib = lib
+    return _comm_lib
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -230,4 +255,6 @@ def loaded_libraries() -> list[str]:
         out.append(_build.HOST_LIB)
     if _hip_lib is not None:
         out.append(_build.HIP_LIB)
+    if _comm_lib is not None:
+        out.append(_build.COMM_LIB)
     return out

@@ -15,6 +15,8 @@ unorderedDataVariant.cu:138-143); without ``-g`` the local rank picks the device
 (the reference would put every rank on GPU 0).
 
 The process group is RCCL (``nccl``) for GPU runs and gloo for CPU runs.
+``LSKNN_DIST_BACKEND=rccl`` uses the native RCCL communicator instead (parallel/rccl.py:
+RCCL called from C++ on the pipeline's own streams; a gloo group for control).
 ``LSKNN_DIST_BACKEND=gloo`` forces gloo with GPU data (collectives staged through host
 memory, see TorchComm): the only way to run several GPU ranks on one device, since RCCL
 refuses two ranks on the same GPU.
@@ -125,8 +127,19 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = datetime.timedelta(seconds=F.timeout_s())
         backend = os.environ.get("LSKNN_DIST_BACKEND", "nccl" if use_gpu else "gloo")
-        if backend not in ("nccl", "gloo"):
-            raise ValueError(f"LSKNN_DIST_BACKEND must be nccl or gloo, not {backend!r}")
+        if backend not in ("nccl", "gloo", "rccl"):
+            raise ValueError(f"LSKNN_DIST_BACKEND must be nccl, rccl or gloo, not {backend!r}")
+        if backend == "rccl":
+            # native RCCL communicator (parallel/rccl.py); a gloo group carries the store,
+            # the watchdog and host-side control
+            if not use_gpu:
+                raise ValueError("LSKNN_DIST_BACKEND=rccl needs a GPU run")
+            from .rccl import RcclComm
+            dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
+            store = dist.distributed_c10d._get_default_store()
+            comm = RcclComm(device, rank, size, store, force=force_distributed)
+            watchdog = F.Watchdog(rank, size, store).start()
+            return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
         if backend == "nccl":
             if not use_gpu:
                 raise ValueError("LSKNN_DIST_BACKEND=nccl needs a GPU run")
@@ -178,6 +191,9 @@ def finalize(launch: Launch) -> None:
         launch.watchdog.stop()
     if dist.is_initialized():
         launch.comm.barrier()
+        inner = getattr(launch.comm, "inner", launch.comm)
+        if hasattr(inner, "destroy"):  # native RCCL communicator
+            inner.destroy()
         dist.destroy_process_group()
 
 

@@ -60,18 +60,22 @@ def test_bench_single_gpu_graph_and_eager(graph):
 
 
 @pytest.mark.gpu
-def test_bench_forced_rccl_single_gpu():
+@pytest.mark.parametrize("backend", ["nccl", "rccl"])
+def test_bench_forced_rccl_single_gpu(backend):
     """One rank through the multi-rank pipeline on a real 1-rank RCCL group: every
-    collective of the step (all-reduce, all-gather, all-to-all-v) runs on RCCL."""
+    collective of the step (all-reduce, all-gather, all-to-all-v) runs on RCCL — through
+    torch.distributed ("nccl") or the native communicator ("rccl", parallel/rccl.py)."""
     out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
                           "--force-dist"], cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1",
-                                                               MASTER_PORT=str(_free_port())),
+                                                               MASTER_PORT=str(_free_port()),
+                                                               LSKNN_DIST_BACKEND=backend),
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = _json_line(out.stdout)
     assert rec["config"]["hip_graph"] is False
     assert rec["config"]["sampled_exact"] == "256/256"
     assert "alltoallv_points" in rec["detail"]["phase_ms_max_over_ranks"]
+    assert rec["config"]["comm"] == backend
 
 
 @pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])

@@ -101,3 +101,64 @@ def test_count_below_gpu_equals_cpu():
     gpu.zero_()
     V.count_below(pts.cuda(), q.cuda(), thr.cuda(), gpu)
     assert torch.equal(gpu.cpu(), cpu)
+
+
+def _native_worker(rank, lib, out_dir):
+    import torch.distributed as dist
+
+    from mpi_cuda_largescaleknn_amd.models import knn_engine as E
+    from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL
+    from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA
+    from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm
+    from mpi_cuda_largescaleknn_amd.parallel.rccl import RcclComm
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    path = None if lib == "rocm" else os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    comm = RcclComm(dev, 0, 1, dist.HashStore(), force=True, lib_path=path)
+    one = SingleComm(dev)
+    res = {"version": comm.version, "path": comm.lib_path}
+    t = torch.tensor([3.0, -1.0, 7.0], device=dev)
+    comm.allreduce_(t, "max")
+    res["allreduce"] = t.cpu()
+    res["allgather"] = comm.allgather(torch.arange(6, dtype=torch.int64, device=dev)).cpu()
+    rows = torch.arange(30, dtype=torch.float32, device=dev).view(10, 3)
+    res["alltoallv"] = comm.alltoallv(rows, [10])[0].cpu()
+    res["p2p"] = comm.p2p([(0, rows)], [(0, (10, 3), torch.float32)])[0].cpu()
+    comm.barrier()
+    p = clustered(60000, seed=12).to(dev)
+    cfg = E.KnnConfig(k=24)
+    for name, fn in (("unordered", PL.unordered_knn), ("prepartitioned", PL.prepartitioned_knn),
+                     ("ring", RA.ring_knn), ("peer", RA.peer_knn)):
+        res[name] = fn(p, comm, cfg).cpu()
+        res[name + "_single"] = fn(p, one, cfg).cpu()
+    big = torch.arange(400_000_000, dtype=torch.int32, device=dev).view(-1, 4)  # 1.6 GB, in pieces
+    got, _ = comm.alltoallv(big, [big.shape[0]])
+    res["big_equal"] = bool(torch.equal(got, big))
+    del got
+    comm.max_msg_bytes = 2 << 30  # probe: one 1.6 GB message (RCCL 2.26 corrupts > 1 GiB)
+    got, _ = comm.alltoallv(big, [big.shape[0]])
+    res["big_unpieced_equal"] = bool(torch.equal(got, big))
+    torch.cuda.synchronize()
+    comm.destroy()
+    torch.save(res, os.path.join(out_dir, "res.pt"))
+
+
+@pytest.mark.parametrize("lib", ["rocm", "torch"])
+def test_native_rccl_comm_forced_one_rank(lib, tmp_path):
+    """parallel/rccl.RcclComm (RCCL called from C++ on the caller's stream), 1-rank
+    forced: raw collectives, every pipeline equal to the single-rank result, a 1.6 GB
+    exchange in pieces; for ROCm's RCCL 2.27 and torch's 2.26. Also records whether one
+    unpieced 1.6 GB message survives (printed; 2.26 is known not to)."""
+    mp.spawn(_native_worker, args=(lib, str(tmp_path)), nprocs=1, join=True)
+    res = torch.load(tmp_path / "res.pt", weights_only=True)
+    print(f"RCCL {res['version']} ({res['path']}): unpieced 1.6 GB message exact = {res['big_unpieced_equal']}")
+    assert torch.equal(res["allreduce"], torch.tensor([3.0, -1.0, 7.0]))
+    assert torch.equal(res["allgather"], torch.arange(6)[None])
+    rows = torch.arange(30, dtype=torch.float32).view(10, 3)
+    assert torch.equal(res["alltoallv"], rows) and torch.equal(res["p2p"], rows)
+    for name in ("unordered", "prepartitioned", "ring", "peer"):
+        assert torch.equal(res[name], res[name + "_single"]), name
+    assert res["big_equal"]
+    if lib == "rocm":
+        assert res["version"] >= 22700
