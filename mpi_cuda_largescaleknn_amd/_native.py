@@ -230,6 +230,7 @@ def comm() -> C.CDLL:
                 lib.lsk_comm_unique_id.argtypes = [C.c_char_p, i32]
                 lib.lsk_comm_init.argtypes = [C.c_char_p, i32, i32, i32, C.POINTER(vp)]
                 lib.lsk_comm_destroy.argtypes = [vp, i32]
+                lib.lsk_comm_async_error.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_char_p)]
                 lib.lsk_comm_allreduce.argtypes = [vp, vp, i64, i32, i32, vp]
                 lib.lsk_comm_allgather.argtypes = [vp, vp, vp, i64, vp]
                 lib.lsk_comm_alltoallv.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, i64, i32, vp]

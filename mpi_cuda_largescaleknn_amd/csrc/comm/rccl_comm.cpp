@@ -35,6 +35,7 @@ struct Api {
   decltype(&ncclCommInitRank) commInitRank = nullptr;
   decltype(&ncclCommDestroy) commDestroy = nullptr;
   decltype(&ncclCommAbort) commAbort = nullptr;
+  decltype(&ncclCommGetAsyncError) asyncError = nullptr;
   decltype(&ncclGetErrorString) errorString = nullptr;
   decltype(&ncclAllReduce) allReduce = nullptr;
   decltype(&ncclAllGather) allGather = nullptr;
@@ -117,6 +118,7 @@ int lsk_comm_load(const char *path) {
   const bool ok = sym(h, "ncclGetVersion", a.getVersion) && sym(h, "ncclGetUniqueId", a.getUniqueId) &&
                   sym(h, "ncclCommInitRank", a.commInitRank) && sym(h, "ncclCommDestroy", a.commDestroy) &&
                   sym(h, "ncclCommAbort", a.commAbort) && sym(h, "ncclGetErrorString", a.errorString) &&
+                  sym(h, "ncclCommGetAsyncError", a.asyncError) &&
                   sym(h, "ncclAllReduce", a.allReduce) && sym(h, "ncclAllGather", a.allGather) &&
                   sym(h, "ncclSend", a.send) && sym(h, "ncclRecv", a.recv) &&
                   sym(h, "ncclGroupStart", a.groupStart) && sym(h, "ncclGroupEnd", a.groupEnd);
@@ -163,6 +165,17 @@ int lsk_comm_destroy(void *comm, int abort) {
   } else {
     LSK_NCCL(g_api.commDestroy((ncclComm_t)comm), "ncclCommDestroy");
   }
+  return 0;
+}
+
+// Asynchronous communicator error (a peer died, a network/xGMI failure): polled by the
+// watchdog thread (ncclCommGetAsyncError is thread-safe); *msg gets RCCL's error string.
+int lsk_comm_async_error(void *comm, int *err, const char **msg) {
+  if (need_api() || !comm) return 1;
+  ncclResult_t r = ncclSuccess;
+  LSK_NCCL(g_api.asyncError((ncclComm_t)comm, &r), "ncclCommGetAsyncError");
+  *err = (int)r;
+  *msg = g_api.errorString(r);
   return 0;
 }
 

@@ -33,6 +33,7 @@ from .comm import Comm
 ABORT_KEY = "lsknn/abort"
 EXIT_PEER_ABORT = 3
 EXIT_TIMEOUT = 124
+EXIT_COMM_ERROR = 5  # the communicator reported an asynchronous error
 
 
 class InjectedFault(RuntimeError):
@@ -140,9 +141,15 @@ class MonitoredComm(Comm):
 class Watchdog:
     """Per-rank daemon thread: peer-abort polling + progress timeout (see module doc)."""
 
-    def __init__(self, rank: int, size: int, store=None, timeout: float | None = None, poll: float = 0.5):
+    def __init__(self, rank: int, size: int, store=None, timeout: float | None = None, poll: float = 0.5,
+                 comm_check=None, on_abort=None):
+        """`comm_check()` -> error string or None: polled every interval (the native RCCL
+        communicator's ncclCommGetAsyncError); `on_abort()` runs before the process exits
+        on any watchdog abort (ncclCommAbort)."""
         self.rank, self.size = rank, size
         self.store = store
+        self.comm_check = comm_check
+        self.on_abort = on_abort
         self.timeout = timeout_s() if timeout is None else timeout
         self.poll = poll
         self._stop = threading.Event()
@@ -157,6 +164,11 @@ class Watchdog:
         self._stop.set()
 
     def _die(self, msg: str, code: int) -> None:
+        if self.on_abort is not None:
+            try:
+                self.on_abort()
+            except Exception:  # noqa: BLE001 - exiting anyway
+                pass
         sys.stderr.write(f"#{self.rank}/{self.size}: {msg}\n")
         sys.stderr.flush()
         sys.stdout.flush()
@@ -173,6 +185,18 @@ class Watchdog:
                 except Exception:  # noqa: BLE001 - store gone = rank 0 (the store host) died
                     if not self._stop.is_set():
                         self._die("aborting: lost the rendezvous store (a peer died)", EXIT_PEER_ABORT)
+            if self.comm_check is not None:
+                try:
+                    err = self.comm_check()
+                except Exception as e:  # noqa: BLE001
+                    err = f"communicator check failed: {e}"
+                if err and not self._stop.is_set():
+                    if self.store is not None:
+                        try:
+                            self.store.set(ABORT_KEY, f"rank {self.rank}: {err}")
+                        except Exception:  # noqa: BLE001
+                            pass
+                    self._die(f"aborting: {err}", EXIT_COMM_ERROR)
             idle = time.monotonic() - HEARTBEAT.t
             if idle > self.timeout and not self._stop.is_set():
                 if self.store is not None:

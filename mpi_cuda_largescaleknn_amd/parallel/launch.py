@@ -138,7 +138,7 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
             dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
             store = dist.distributed_c10d._get_default_store()
             comm = RcclComm(device, rank, size, store, force=force_distributed)
-            watchdog = F.Watchdog(rank, size, store).start()
+            watchdog = F.Watchdog(rank, size, store, comm_check=comm.async_error, on_abort=comm.abort).start()
             return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
         if backend == "nccl":
             if not use_gpu:

@@ -99,6 +99,26 @@ class RcclComm(Comm):
             _check(_native.comm().lsk_comm_destroy(self._h, int(abort)), "ncclCommDestroy")
             self._h = None
 
+    def async_error(self) -> str | None:
+        """RCCL's asynchronous error state (None while healthy); safe from another thread
+        (the watchdog polls it)."""
+        h = getattr(self, "_h", None)
+        if not h:
+            return None
+        err, msg = C.c_int(0), C.c_char_p()
+        if _native.comm().lsk_comm_async_error(h, C.byref(err), C.byref(msg)) != 0:
+            return "ncclCommGetAsyncError failed"
+        if err.value == 0:
+            return None
+        return f"RCCL async error {err.value}: {msg.value.decode() if msg.value else ''}"
+
+    def abort(self) -> None:
+        """ncclCommAbort: unblocks this rank's pending RCCL work before the process exits."""
+        h = getattr(self, "_h", None)
+        if h:
+            self._h = None
+            _native.comm().lsk_comm_destroy(h, 1)
+
     # ---------------------------------------------------------------- collectives
     def _dev(self, t: torch.Tensor) -> torch.Tensor:
         return t if t.device == self._device else t.to(self._device)

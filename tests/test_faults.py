@@ -90,3 +90,28 @@ def test_rank_count_mismatch_message(pts, tmp_path):
     p, _ = _run([PRE, str(lst), "-o", str(tmp_path / "out"), "-k", "8", "--device", "cpu"], 2)
     assert p.returncode != 0
     assert "number of input files does not match MPI size" in p.stderr
+
+
+def test_watchdog_aborts_on_communicator_error(tmp_path):
+    """The watchdog polls the communicator's asynchronous error state (native RCCL:
+    ncclCommGetAsyncError); on an error it runs the abort hook (ncclCommAbort) and the
+    rank exits with EXIT_COMM_ERROR."""
+    import subprocess
+    import sys
+
+    flag = tmp_path / "aborted"
+    code = (
+        "import time\n"
+        "from mpi_cuda_largescaleknn_amd.parallel import faults as F\n"
+        "n = [0]\n"
+        "def check():\n"
+        "    n[0] += 1\n"
+        "    return 'RCCL async error 6: remote process exited' if n[0] >= 3 else None\n"
+        f"F.Watchdog(0, 2, None, timeout=60, poll=0.05, comm_check=check,\n"
+        f"           on_abort=lambda: open({str(flag)!r}, 'w').write('x')).start()\n"
+        "time.sleep(30)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=root)
+    assert out.returncode == 5, (out.returncode, out.stderr)
+    assert "remote process exited" in out.stderr
+    assert flag.exists()
