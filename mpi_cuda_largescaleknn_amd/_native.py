@@ -149,7 +149,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_tree_nodes": ([i64], i64),
         "lsk_hip_build_tree": ([vp, i64, vp, vp, vp], i32),
         "lsk_hip_tree_set_radii": ([vp, i64, vp, vp], i32),
-        "lsk_hip_tree_set_radii_ub": ([vp, i64, i32, vp], i32),
+        "lsk_hip_tree_set_radii_ub": ([vp, vp, i64, i32, vp], i32),
         "lsk_hip_knn_exact": ([C.POINTER(KnnArgs), vp, vp, i64, vp], i32),
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),

@@ -79,8 +79,9 @@ int lsk_hip_build_tree(const float *sorted_pts, int64_t n, float *nodes, float *
                        void *stream);
 // leaves' lo.w = max over the bucket's queries of d2[i]; propagated to all levels.
 int lsk_hip_tree_set_radii(float *nodes, int64_t n, const float *d2_sorted, void *stream);
-// a-priori upper bound of each node's k-th squared radius (from bucket boxes only)
-int lsk_hip_tree_set_radii_ub(float *nodes, int64_t n, int k, void *stream);
+// a-priori upper bound of each node's k-th squared radius (from the sorted points and
+// bucket boxes only, before any query ran)
+int lsk_hip_tree_set_radii_ub(float *nodes, const float *sorted_pts, int64_t n, int k, void *stream);
 
 // ---- k-th-distance selection ----------------------------------------------------------
 typedef struct lsk_tree_view {

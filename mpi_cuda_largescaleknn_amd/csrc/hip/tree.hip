@@ -113,16 +113,24 @@ __global__ __launch_bounds__(256) void leaf_radius_kernel(const float *__restric
 }
 
 // A-priori upper bound of every leaf's k-th squared radius, before any k-NN runs (the
-// overlapped halo exchange publishes it while the local k-NN is still running): the
+// overlapped halo exchange publishes it while the local k-NN is still running). The
 // W = ceil(k/64) + 1 consecutive buckets around the leaf hold >= k points (the query
-// itself included), so no query of the leaf has its k-th neighbour farther than the
-// farthest corner pair of the leaf box and the window's union box. Padded by 2^-16
-// relative (far above the rounding of the canonical d2 the kernels compare). n < k:
-// +inf (fewer than k local points: the local k-th is infinite).
-__global__ __launch_bounds__(256) void leaf_radius_ub_kernel(int64_t n, int k, float *__restrict__ nodes,
-                                                             int depth, int64_t nleaf_slots) {
-  const int64_t leaf = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// itself included). For a window point p let m(p) = the farthest-corner distance from p
+// to the leaf box: every query q of the leaf has |q - p| <= m(p), so the k-th smallest
+// m(p) over the window bounds every query's k-th neighbour distance. One wave per leaf,
+// W values per lane, k-th smallest by bisection on the float bits (ballot counts).
+// Beyond kUbMaxW buckets (k > 448) the cheaper, looser farthest-corner pair of the leaf
+// box and the window's union box is used. Padded by 2^-16 relative (far above the
+// rounding of the canonical d2 the kernels compare). n < k: +inf (fewer than k local
+// points: the local k-th is infinite).
+constexpr int kUbMaxW = 8;
+
+__global__ __launch_bounds__(256) void leaf_radius_ub_kernel(const float *__restrict__ pts, int64_t n, int k,
+                                                             float *__restrict__ nodes, int depth,
+                                                             int64_t nleaf_slots) {
+  const int64_t leaf = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (leaf >= nleaf_slots) return;
+  const int lane = lsk::lane_id();
   const int64_t nb = (n + lsk::kBucket - 1) / lsk::kBucket;
   const int64_t slots = (int64_t)1 << depth;
   const float4 *nd = (const float4 *)nodes;
@@ -134,29 +142,54 @@ __global__ __launch_bounds__(256) void leaf_radius_ub_kernel(int64_t n, int k, f
       const int64_t W = min(nb, (int64_t)(k + lsk::kBucket - 1) / lsk::kBucket + 1);
       int64_t st = leaf - (W - 1) / 2;
       st = st < 0 ? 0 : (st > nb - W ? nb - W : st);
-      const float inf = __builtin_inff();
-      float wlx = inf, wly = inf, wlz = inf, whx = -inf, why = -inf, whz = -inf;
-      for (int64_t b = st; b < st + W; b++) {
-        const float4 lo = nd[2 * (slots + b)], hi = nd[2 * (slots + b) + 1];
-        wlx = fminf(wlx, lo.x); wly = fminf(wly, lo.y); wlz = fminf(wlz, lo.z);
-        whx = fmaxf(whx, hi.x); why = fmaxf(why, hi.y); whz = fmaxf(whz, hi.z);
-      }
       const float4 lo = nd[2 * (slots + leaf)], hi = nd[2 * (slots + leaf) + 1];
-      const float ex = fmaxf(whx - lo.x, hi.x - wlx), ey = fmaxf(why - lo.y, hi.y - wly),
-                  ez = fmaxf(whz - lo.z, hi.z - wlz);
-      r = lsk::dist2(ex, ey, ez) * (1.f + 0x1p-16f);
+      if (W <= kUbMaxW) {
+        uint32_t v[kUbMaxW];
+#pragma unroll
+        for (int j = 0; j < kUbMaxW; j++) {
+          const int64_t i = (st + j) * lsk::kBucket + lane;
+          v[j] = 0xffffffffu;
+          if (j < W && i < n) {
+            const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
+            const float ex = fmaxf(px - lo.x, hi.x - px), ey = fmaxf(py - lo.y, hi.y - py),
+                        ez = fmaxf(pz - lo.z, hi.z - pz);
+            v[j] = __float_as_uint(lsk::dist2(ex, ey, ez));
+          }
+        }
+        uint32_t sel = 0;  // largest value with count(v < sel) < k = the k-th smallest
+        for (int b = 31; b >= 0; --b) {
+          const uint32_t cand = sel | (1u << b);
+          uint32_t c = 0;
+#pragma unroll
+          for (int j = 0; j < kUbMaxW; j++) c += (uint32_t)__popcll(__ballot(v[j] < cand));
+          if (c < (uint32_t)k) sel = cand;
+        }
+        r = __uint_as_float(sel);
+      } else {
+        const float inf = __builtin_inff();
+        float wlx = inf, wly = inf, wlz = inf, whx = -inf, why = -inf, whz = -inf;
+        for (int64_t b = st; b < st + W; b++) {
+          const float4 bl = nd[2 * (slots + b)], bh = nd[2 * (slots + b) + 1];
+          wlx = fminf(wlx, bl.x); wly = fminf(wly, bl.y); wlz = fminf(wlz, bl.z);
+          whx = fmaxf(whx, bh.x); why = fmaxf(why, bh.y); whz = fmaxf(whz, bh.z);
+        }
+        const float ex = fmaxf(whx - lo.x, hi.x - wlx), ey = fmaxf(why - lo.y, hi.y - wly),
+                    ez = fmaxf(whz - lo.z, hi.z - wlz);
+        r = lsk::dist2(ex, ey, ez);
+      }
+      r *= 1.f + 0x1p-16f;
     }
   }
-  nodes[8 * (slots + leaf) + 3] = r;
+  if (lane == 0) nodes[8 * (slots + leaf) + 3] = r;
 }
 
 }  // namespace
 
-extern "C" int lsk_hip_tree_set_radii_ub(float *nodes, int64_t n, int k, void *stream) {
+extern "C" int lsk_hip_tree_set_radii_ub(float *nodes, const float *sorted_pts, int64_t n, int k, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   const int depth = lsk_hip_tree_depth(n);
   const int64_t slots = (int64_t)1 << depth;
-  leaf_radius_ub_kernel<<<lsk_blocks(slots, 256), 256, 0, s>>>(n, k, nodes, depth, slots);
+  leaf_radius_ub_kernel<<<lsk_blocks(slots, 4), 256, 0, s>>>(sorted_pts, n, k, nodes, depth, slots);
   LSK_CHECK_LAUNCH("tree_leaf_radius_ub");
   for (int l = depth - 1; l >= 0; l--) {
     levelup_kernel<<<lsk_blocks((int64_t)1 << l, 256), 256, 0, s>>>(nodes, l, 1);

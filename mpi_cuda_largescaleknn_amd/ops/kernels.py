@@ -335,13 +335,19 @@ def kth_cpu(points: torch.Tensor, queries: torch.Tensor, k: int, cut2: float, me
 
 
 # --------------------------------------------------------------------------- halo
-def tree_set_radii_ub(nodes: torch.Tensor, n: int, k: int) -> torch.Tensor:
-    """Per-node upper bound of the k-th squared radius before any query ran: the
-    ceil(k/64)+1 buckets around each leaf hold >= k points, so a leaf's k-th neighbour
-    lies within the farthest corner pair of its box and their union box (tree.hip
-    leaf_radius_ub_kernel; same arithmetic here)."""
+UB_MAX_W = 8  # tree.hip kUbMaxW: beyond it the box-pair bound
+
+
+def tree_set_radii_ub(nodes: torch.Tensor, pts: torch.Tensor, n: int, k: int) -> torch.Tensor:
+    """Per-node upper bound of the k-th squared radius before any query ran (tree.hip
+    leaf_radius_ub_kernel): the ceil(k/64)+1 buckets around a leaf hold >= k points;
+    with m(p) = farthest-corner distance from window point p to the leaf box, the k-th
+    smallest m(p) bounds every leaf query's k-th neighbour distance (beyond UB_MAX_W
+    buckets: the farthest corner pair of the leaf box and the window's union box).
+    `pts`: the index's sorted points."""
     if is_gpu(nodes):
-        check(_native.hip().lsk_hip_tree_set_radii_ub(_ptr(nodes), n, k, _stream(nodes)), "tree_set_radii_ub")
+        check(_native.hip().lsk_hip_tree_set_radii_ub(_ptr(nodes), _ptr(pts), n, k, _stream(nodes)),
+              "tree_set_radii_ub")
         return nodes
     depth = tree_depth(n)
     slots = 1 << depth
@@ -355,11 +361,20 @@ def tree_set_radii_ub(nodes: torch.Tensor, n: int, k: int) -> torch.Tensor:
         st = (leaf - (w - 1) // 2).clamp(0, nb - w)
         lo = nodes[slots:slots + nb, 0:3]
         hi = nodes[slots:slots + nb, 4:7]
-        win = st[:, None] + torch.arange(w)[None, :]
-        wlo = lo[win].amin(dim=1)
-        whi = hi[win].amax(dim=1)
-        e = torch.maximum(whi - lo, hi - wlo)
-        d2 = torch.addcmul(torch.addcmul(e[:, 0] * e[:, 0], e[:, 1], e[:, 1]), e[:, 2], e[:, 2])
+        if w <= UB_MAX_W:
+            idx = (st[:, None] * BUCKET + torch.arange(w * BUCKET)[None, :])   # [nb, 64w]
+            valid = idx < n
+            p = pts[:n][idx.clamp(max=n - 1)]                                   # [nb, 64w, 3]
+            e = torch.maximum(p - lo[:, None, :], hi[:, None, :] - p)
+            m = torch.addcmul(torch.addcmul(e[..., 0] * e[..., 0], e[..., 1], e[..., 1]), e[..., 2], e[..., 2])
+            m = torch.where(valid, m, torch.full_like(m, math.inf))
+            d2 = m.kthvalue(k, dim=1).values
+        else:
+            win = st[:, None] + torch.arange(w)[None, :]
+            wlo = lo[win].amin(dim=1)
+            whi = hi[win].amax(dim=1)
+            e = torch.maximum(whi - lo, hi - wlo)
+            d2 = torch.addcmul(torch.addcmul(e[:, 0] * e[:, 0], e[:, 1], e[:, 1]), e[:, 2], e[:, 2])
         r[:nb] = d2 * (1.0 + 2.0 ** -16)
     nodes[slots:, 3] = r
     for level in range(depth - 1, -1, -1):

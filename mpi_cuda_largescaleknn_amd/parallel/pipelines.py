@@ -458,7 +458,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         info.timer.mark("knn_local")
         return halo_refine(index, d2, comm, cfg, hint2, info, final_out=final_out)
     if not gpu:  # same data flow, no streams to overlap on
-        ub = K.tree_set_radii_ub(index.nodes.clone(), index.n, cfg.k)
+        ub = K.tree_set_radii_ub(index.nodes.clone(), index.pts, index.n, cfg.k)
         recv = _halo_send(index, ub, comm, cfg, info, marks=False)
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
         info.timer.mark("knn_local+halo_exchange")
@@ -474,7 +474,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True, deferred=pend)
     with torch.cuda.stream(side):
         ub = index.nodes.clone()
-        K.tree_set_radii_ub(ub, index.n, cfg.k)
+        K.tree_set_radii_ub(ub, index.pts, index.n, cfg.k)
         recv = _halo_send(index, ub, comm, cfg, info, marks=False)
     cur.wait_stream(comp)
     cur.wait_stream(side)

@@ -175,3 +175,23 @@ def test_overlapped_halo_gpu_equals_sequential(k, monkeypatch):
     assert torch.equal(res[True][0], ref) and torch.equal(res[False][0], ref)
     assert res[True][1] >= res[False][1]
     assert res[True][2] == [1, 1, 1, 1] and res[False][2] == [0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("k", [1, 100, 448, 600])
+def test_radius_upper_bound_gpu(k):
+    """tree.hip leaf_radius_ub_kernel: every leaf's a-priori bound covers the k-th squared
+    distance of all its queries (GPU k-NN), and matches the CPU formula closely
+    (k = 600: the box-pair fallback beyond 8 window buckets)."""
+    p = clustered(100_000, seed=k).to(DEV)
+    idx = E.build_index(p)
+    n = idx.n
+    ub = K.tree_set_radii_ub(idx.nodes.clone(), idx.pts, n, k)
+    d2 = E.query(idx, E.KnnConfig(k=k), E.radius_hint(idx.box, n, k))
+    slots = 1 << idx.depth
+    nb = (n + 63) // 64
+    leaf_max = torch.zeros(slots * 64, device=DEV)
+    leaf_max[:n] = d2
+    leaf_max = leaf_max.view(slots, 64).amax(dim=1)
+    assert bool((ub[slots:slots + nb, 3] >= leaf_max[:nb]).all())
+    cpu = K.tree_set_radii_ub(idx.nodes.cpu().clone(), idx.pts.cpu(), n, k)
+    assert torch.allclose(cpu[slots:slots + nb, 3], ub[slots:slots + nb, 3].cpu(), rtol=1e-5)

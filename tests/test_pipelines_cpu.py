@@ -301,10 +301,10 @@ def test_overlapped_halo_superset_and_exact(k, monkeypatch):
 
 def test_radius_upper_bound_covers_kth():
     """Every leaf's a-priori bound >= the largest k-th squared distance of its queries."""
-    for n, k in ((5000, 1), (5000, 64), (5000, 65), (3000, 200), (100, 100), (50, 100)):
+    for n, k in ((5000, 1), (5000, 64), (5000, 65), (3000, 200), (100, 100), (50, 100), (6000, 500)):
         p = uniform(n, seed=n + k)
         idx = E.build_index(p)
-        nodes = K.tree_set_radii_ub(idx.nodes.clone(), idx.n, k)
+        nodes = K.tree_set_radii_ub(idx.nodes.clone(), idx.pts, idx.n, k)
         d2 = K.kth_cpu(idx.pts[:n], idx.pts[:n], k, math.inf)
         slots = 1 << idx.depth
         nb = (n + 63) // 64
