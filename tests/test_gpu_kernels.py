@@ -390,3 +390,15 @@ def test_mfma_screen_is_conservative(dist):
         d2 = ((q[:, None, :] - cand) ** 2).sum(-1)
         tot += int((d2 < t[:, None]).sum())
     assert abs(tot - outs[0]) <= max(8, tot // 100000), (tot, outs[0])
+
+
+@pytest.mark.parametrize("n", [1, 1023, 1024, 1025, 300_001])
+def test_gather3_tiled_equals_indexing(n):
+    """util.hip gather3 (LDS-tiled, coalesced float4 stores, partial last tile) vs torch
+    indexing, with padding rows untouched."""
+    g = torch.Generator().manual_seed(n)
+    src = torch.rand((n + 17, 3), generator=g).to(DEV)
+    idx = torch.randperm(n + 17, generator=g)[:n].to(torch.int32).to(DEV)
+    got = K.gather3(src, idx, pad=5)
+    assert torch.equal(got[:n].cpu(), src.cpu()[idx.long().cpu()])
+    assert torch.equal(got[n:].cpu(), torch.zeros(5, 3))
