@@ -447,6 +447,15 @@ def _overlap_streams(dev: torch.device):
     return st
 
 
+def _radius_bounds(index: E.LocalIndex, cfg: E.KnnConfig) -> torch.Tensor:
+    """A copy of the tree with a-priori per-node k-th squared radius bounds, capped at the
+    cutoff (-r): candidates at or beyond it are never counted, so no query needs them."""
+    ub = K.tree_set_radii_ub(index.nodes.clone(), index.pts, index.n, cfg.k)
+    if math.isfinite(cfg.cut2):
+        ub[:, 3].clamp_(max=cfg.cut2 * (1.0 + 2.0 ** -16))
+    return ub
+
+
 def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: float | torch.Tensor,
                   info: RunInfo, final_out: torch.Tensor) -> torch.Tensor:
     """Local k-NN of every owned query + halo exchange + re-query (distributed runs).
@@ -458,8 +467,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         info.timer.mark("knn_local")
         return halo_refine(index, d2, comm, cfg, hint2, info, final_out=final_out)
     if not gpu:  # same data flow, no streams to overlap on
-        ub = K.tree_set_radii_ub(index.nodes.clone(), index.pts, index.n, cfg.k)
-        recv = _halo_send(index, ub, comm, cfg, info, marks=False)
+        recv = _halo_send(index, _radius_bounds(index, cfg), comm, cfg, info, marks=False)
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
         info.timer.mark("knn_local+halo_exchange")
         K.tree_set_radii(index.nodes, index.n, d2)
@@ -473,9 +481,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
     with torch.cuda.stream(comp):
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True, deferred=pend)
     with torch.cuda.stream(side):
-        ub = index.nodes.clone()
-        K.tree_set_radii_ub(ub, index.pts, index.n, cfg.k)
-        recv = _halo_send(index, ub, comm, cfg, info, marks=False)
+        recv = _halo_send(index, _radius_bounds(index, cfg), comm, cfg, info, marks=False)
     cur.wait_stream(comp)
     cur.wait_stream(side)
     recv.record_stream(cur)

@@ -314,3 +314,23 @@ def test_radius_upper_bound_covers_kth():
         ub = nodes[slots:slots + nb, 3]
         assert bool((ub >= leaf_max[:nb]).all()), (n, k)
         assert float(nodes[1, 3]) >= float(d2.max())
+
+
+def test_overlapped_halo_cutoff_caps_bounds(monkeypatch):
+    """With -r the a-priori bounds are capped at the cutoff: a small radius sends a much
+    smaller halo than no radius, results stay exact."""
+    p = uniform(12000, seed=3)
+    k = 20
+    res = {}
+    for r in (math.inf, 0.02):
+        cfg = E.KnnConfig(k=k, max_radius=r, publish_levels=4)
+        infos = [PL.RunInfo(PL.PhaseTimer(False, torch.device("cpu"))) for _ in range(4)]
+
+        def fn(comm):
+            b, e = block(p.shape[0], comm.rank, comm.size)
+            return PL.unordered_knn(p[b:e], comm, cfg, infos[comm.rank])
+
+        out = torch.cat(run_loopback(4, fn))
+        assert torch.equal(out, oracle(p, k, r))
+        res[r] = sum(i.counts.get("halo_recv", 0) for i in infos)
+    assert res[0.02] < res[math.inf] / 2, res
