@@ -170,15 +170,15 @@ struct WaveLdsR {
 struct Lane {
   float qx, qy, qz;
   uint32_t state;
-  uint32_t lo_b, hi_b, shift;
+  uint32_t lo_b, hi_b, shift;  // histogram range; lo_b = the answer once DONE
   int32_t bin_hi;
   uint32_t c_hi;
   uint32_t c_base;  // exact count of values < lo_b, or kUnknown
   uint32_t nudf;    // underflow retries so far
-  uint32_t cut_lim;
-  uint32_t band_lo, band_w, m, bc;
+  uint32_t band_lo, band_w, bc;  // (READY: c_base holds the count below the band)
   uint32_t coff, ccnt;
-  uint32_t ans;
+  // (no separate answer register: once a lane is DONE — or READY and collected — its
+  // lo_b is dead and holds the answer bits, see done())
 #ifdef LSK_PROFILE
   uint32_t pdead, pslots;  // HIST candidate slots with no lane in range / all slots
   bool pband;              // COLLECT: this lane had a value in its band this step
@@ -1299,15 +1299,15 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) r_est2 = 1.f;
 
   const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
-  s.cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
-  s.band_lo = s.band_w = s.m = s.bc = s.coff = s.ccnt = 0;
+  // cutoff bits: wave-uniform (an SGPR, not a per-lane field)
+  const uint32_t cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
+  s.band_lo = s.band_w = s.bc = s.coff = s.ccnt = 0;
   // every lane's histogram state is defined (lanes that never histogram included:
   // the wave-wide shrink step reads bin_hi / c_hi of all lanes)
   s.lo_b = s.hi_b = s.shift = s.c_hi = 0;
   s.bin_hi = 0;
   s.c_base = 0;
   s.nudf = 0;
-  s.ans = cut_b;
 #ifdef LSK_PROFILE
   s.pdead = s.pslots = 0;
   s.pband = false;
@@ -1320,6 +1320,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   if (!valid || total_pts < (int64_t)k) {
     s.state = ST_DONE;
     s.hi_b = 0;
+    s.lo_b = cut_b;
     qs |= QS_DONE_CUT;
   } else {
     s.state = ST_HIST;
@@ -1328,7 +1329,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       // known upper bound (re-query): range ends just above it, no overflow possible
       const uint32_t top_b = fbits(ub) + 1u;
       const uint32_t span = (uint32_t)kBins << kShift0;
-      set_range(s, top_b > span ? top_b - span : 0u, kShift0, min(top_b, s.cut_lim), kUnknown);
+      set_range(s, top_b > span ? top_b - span : 0u, kShift0, min(top_b, cut_lim), kUnknown);
     } else {
       const uint32_t est_b = fbits(r_est2);
       const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;  // top kTopBins/8 oct. above
@@ -1337,11 +1338,11 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
         // zero probe: bins of single float bits from 0 (bin 0 = exact zeros); if fewer
         // than k values are that small, the overflow resumes at lo0 (band_lo/band_w are
         // unused while histogramming and carry it)
-        set_range(s, 0u, 0u, s.cut_lim, kUnknown);
+        set_range(s, 0u, 0u, cut_lim, kUnknown);
         s.band_lo = lo0;
         s.band_w = 1u;
       } else {
-        set_range(s, lo0, kShift0, s.cut_lim, kUnknown);
+        set_range(s, lo0, kShift0, cut_lim, kUnknown);
       }
     }
   }
@@ -1360,7 +1361,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
         limit = 1;
         if (s.state != ST_DONE) {
           s.state = ST_DONE;
-          s.ans = kNaNBits;
+          s.lo_b = kNaNBits;
           qs |= QS_LIMIT | QS_FAIL;
         }
         break;
@@ -1406,7 +1407,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
               set_range(s, s.lo_b, sh, s.hi_b, s.c_base);
             }
           } else {
-            set_range(s, s.lo_b, s.shift, s.hi_b > s.lo_b ? s.hi_b : s.cut_lim, s.c_base);
+            set_range(s, s.lo_b, s.shift, s.hi_b > s.lo_b ? s.hi_b : cut_lim, s.c_base);
           }
         }
         continue;
@@ -1419,24 +1420,24 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       bool ovf = false;
       if (s.state == ST_HIST && !hist_consistent(s, W.L->pool, lane)) {
         s.state = ST_DONE;  // a 16-bit bin wrapped: counts are unusable
-        s.ans = kNaNBits;
+        s.lo_b = kNaNBits;
         qs |= QS_BINOVF | QS_FAIL;
       }
       if (s.state == ST_HIST) {
         const uint32_t top = top_count(s, W.L->pool, lane);
         if (s.c_hi < k) {
-          if (s.hi_b >= s.cut_lim) {
+          if (s.hi_b >= cut_lim) {
             s.state = ST_DONE;
-            s.ans = cut_b;
+            s.lo_b = cut_b;
             qs |= QS_DONE_CUT;
           } else {
             ovf = true;
             qs |= QS_OVERFLOW;
             if (s.band_w != 0u && s.band_lo > s.hi_b) {
               // failed zero probe: back to the estimate's range (count below it unknown)
-              set_range(s, s.band_lo, kShift0, s.cut_lim, kUnknown);
+              set_range(s, s.band_lo, kShift0, cut_lim, kUnknown);
             } else {
-              set_range(s, s.hi_b, kShift0, s.cut_lim, s.c_hi);
+              set_range(s, s.hi_b, kShift0, cut_lim, s.c_hi);
             }
             s.band_lo = s.band_w = 0u;
           }
@@ -1453,13 +1454,13 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
           const uint32_t bw = s.hi_b - bl;
           if (bw <= 1u) {
             s.state = ST_DONE;
-            s.ans = bl;
+            s.lo_b = bl;
             qs |= QS_DONE_BAND1;
           } else {
             s.state = ST_READY;
             s.band_lo = bl;
             s.band_w = bw;
-            s.m = k - below;
+            s.c_base = below;  // READY: the count below the band (the band's rank is k - below)
             s.bc = s.c_hi - below;
           }
         }
@@ -1480,7 +1481,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     if (s.state == ST_READY && s.bc > (uint32_t)(kPool / lsk::kWave)) {
       qs |= QS_REFINE;
       const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;  // kBins bins cover the band
-      set_range(s, s.band_lo, sh, s.band_lo + s.band_w, k - s.m);
+      set_range(s, s.band_lo, sh, s.band_lo + s.band_w, s.c_base);
       s.band_lo = s.band_w = 0;
       s.state = ST_HIST;
     }
@@ -1502,7 +1503,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       qs |= QS_COLLECTED;
       if (s.ccnt != s.bc) qs |= QS_MISMATCH | QS_FAIL;
       uint32_t *h = W.L->pool + s.coff;
-      const uint32_t c = min(s.ccnt, s.bc), m = s.m;
+      const uint32_t c = min(s.ccnt, s.bc), m = k - s.c_base;
       if (!(qs & QS_FAIL) && m >= 1 && m <= c) {
         for (int i = (int)(m / 2) - 1; i >= 0; i--) heap_sift(h, (uint32_t)i, m);
         for (uint32_t i = m; i < c; i++) {
@@ -1512,10 +1513,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
             heap_sift(h, 0, m);
           }
         }
-        s.ans = h[0];
+        s.lo_b = h[0];
       } else {
         qs |= QS_MISMATCH | QS_FAIL;
-        s.ans = kNaNBits;
+        s.lo_b = kNaNBits;
       }
     }
     LSK_PADD(W.prof[6], ts0);
@@ -1525,7 +1526,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   if (W.guard) qs |= QS_FAIL;
   if (A.debug_fail_mod > 0 && qi % A.debug_fail_mod == 0) qs |= QS_FAIL;
   const bool failed = valid && (qs & QS_FAIL);
-  if (failed) s.ans = kNaNBits;
+  if (failed) s.lo_b = kNaNBits;
   if (A.fail_count) {
     // failure list: one atomic per wave with failures, lanes write their slots
     const uint64_t fm = __ballot(failed);
@@ -1539,8 +1540,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   }
 
   if (valid) {
-    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.ans));
-    if (A.out_d2) A.out_d2[qi] = bitsf(s.ans);
+    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.lo_b));
+    if (A.out_d2) A.out_d2[qi] = bitsf(s.lo_b);
 #ifdef LSK_PROFILE  // debug: wave cycles (>> 16) in place of the pass count
     if (A.qstatus)
       A.qstatus[qi] = qs | ((uint32_t)min((__builtin_readcyclecounter() - twave0) >> 16, (uint64_t)0xffff) << 16);
