@@ -162,8 +162,11 @@ def main():
         elif args.mode == "peer":
             out = RA.peer_knn(pts, comm, cfg, info)
         elif args.variant == "unordered":
+            # one rank: the kernel writes host_out directly (k >= 48); several ranks: the
+            # grouped result return copies each group's rows into it under the exchange
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
-                                   out=host_out if direct else None)
+                                   out=host_out if (direct or (comm.distributed and device.type == "cuda"))
+                                   else None)
         else:
             out = PL.prepartitioned_knn(pts, comm, cfg, info, out=host_out if direct else None)
         if out.data_ptr() != host_out.data_ptr():

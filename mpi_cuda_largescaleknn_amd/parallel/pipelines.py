@@ -199,6 +199,13 @@ class Redist:
     origin_index: torch.Tensor    # int64: return-receive order -> local input row
     back_counts: list             # rows coming back from each rank
     box: torch.Tensor             # global box of all points (exact)
+    # per stream chunk (grouped return): local input span, send permutation, rows sent
+    # to / received from each rank, first owned row of the chunk
+    spans: list = field(default_factory=list)
+    perms: list = field(default_factory=list)
+    scs: list = field(default_factory=list)
+    rcs: list = field(default_factory=list)
+    bases: list = field(default_factory=list)
 
 
 def redistribute_stream(host_pts: torch.Tensor, comm: Comm, info: RunInfo,
@@ -288,7 +295,9 @@ def redistribute_stream(host_pts: torch.Tensor, comm: Comm, info: RunInfo,
     ret_parts, ret_counts = [[] for _ in range(size)], [0] * size
     orig_parts, back_counts = [[] for _ in range(size)], [0] * size
     base = 0
+    bases = []
     for c, (s, e) in enumerate(spans):
+        bases.append(base)
         ro = _offsets(rcs[c])
         so = _offsets(scs[c])
         for j in range(size):
@@ -305,7 +314,50 @@ def redistribute_stream(host_pts: torch.Tensor, comm: Comm, info: RunInfo,
     info.counts["sent_points"] = sum(sum(sc) - sc[comm.rank] for sc in scs)
     info.counts["owned_points"] = int(owned.shape[0])
     info.counts["stream_chunks"] = len(spans)
-    return Redist(owned, ret_index, ret_counts, origin_index, back_counts, box)
+    return Redist(owned, ret_index, ret_counts, origin_index, back_counts, box,
+                  spans=spans, perms=perms, scs=scs, rcs=rcs, bases=bases)
+
+
+RETURN_GROUPS = 4  # result-return groups of stream chunks (each: all-to-all-v, scatter, D2H)
+
+
+def _return_grouped(R: Redist, dist_owned: torch.Tensor, comm: Comm, res: torch.Tensor,
+                    out: torch.Tensor) -> None:
+    """Result return in groups of stream chunks: group g's all-to-all-v and scatter
+    complete the local rows of its chunks, whose device-to-host copy into the pinned
+    `out` then runs on a copy stream while group g+1 is exchanged (the PCIe copy of the
+    results hides under the xGMI return). Counts are known from the redistribution."""
+    dev = res.device
+    size = comm.size
+    nch = len(R.spans)
+    ng = max(1, min(RETURN_GROUPS, nch))
+    bounds = [nch * g // ng for g in range(ng + 1)]
+    cur = torch.cuda.current_stream(dev)
+    copy_stream = torch.cuda.Stream(dev)
+    empty = torch.zeros(0, dtype=torch.int64, device=dev)
+    for g in range(ng):
+        cs = range(bounds[g], bounds[g + 1])
+        ret, orig, rc, bc = [], [], [0] * size, [0] * size
+        for j in range(size):
+            for c in cs:
+                ro, so = _offsets(R.rcs[c]), _offsets(R.scs[c])
+                if R.rcs[c][j]:
+                    ret.append(torch.arange(R.bases[c] + ro[j], R.bases[c] + ro[j + 1], device=dev))
+                    rc[j] += R.rcs[c][j]
+                if R.scs[c][j]:
+                    orig.append(R.perms[c][so[j]:so[j + 1]].to(torch.int64) + R.spans[c][0])
+                    bc[j] += R.scs[c][j]
+        ret_i = torch.cat(ret) if ret else empty
+        orig_i = torch.cat(orig) if orig else empty
+        back, _ = comm.alltoallv(dist_owned[ret_i], rc, recv_counts=bc)
+        K.scatter1(back, orig_i.to(torch.int32), res, finalize=False)
+        s0, s1 = R.spans[cs[0]][0], R.spans[cs[-1]][1]
+        if s1 > s0:
+            copy_stream.wait_stream(cur)
+            with torch.cuda.stream(copy_stream):
+                out[s0:s1].copy_(res[s0:s1], non_blocking=True)
+    res.record_stream(copy_stream)
+    cur.wait_stream(copy_stream)
 
 
 def _offsets(counts):
@@ -577,6 +629,11 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     knn_with_halo(index, comm, cfg, hint2, info, dist_owned)
     res = torch.empty(n_local, dtype=torch.float32, device=dev)
+    if streamed and out is not None and out.device.type == "cpu" and res.device.type == "cuda" \
+            and RETURN_GROUPS > 1 and len(R.spans) > 1:
+        _return_grouped(R, dist_owned, comm, res, out)
+        info.timer.mark("return")
+        return out
     if streamed:
         # counts of the return are known from the send side: no count exchange
         back, _ = comm.alltoallv(dist_owned[R.ret_index], R.ret_counts, recv_counts=R.back_counts)

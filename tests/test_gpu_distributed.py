@@ -195,3 +195,28 @@ def test_radius_upper_bound_gpu(k):
     assert bool((ub[slots:slots + nb, 3] >= leaf_max[:nb]).all())
     cpu = K.tree_set_radii_ub(idx.nodes.cpu().clone(), idx.pts.cpu(), n, k)
     assert torch.allclose(cpu[slots:slots + nb, 3], ub[slots:slots + nb, 3].cpu(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("groups", [1, 3, 4])
+def test_grouped_return_into_pinned_host(groups, monkeypatch):
+    """Streamed input and a pinned host output: the result return runs in groups of stream
+    chunks, each group's rows copied to the host on a copy stream while the next group is
+    exchanged (groups=1: the single return + copy); bit-identical to one rank."""
+    monkeypatch.setattr(PL, "STREAM_CHUNK", 30_000)
+    monkeypatch.setattr(PL, "RETURN_GROUPS", groups)
+    p = clustered(250_000, seed=groups)
+    k = 50
+    ref = single(p, k)
+
+    def fn(comm):
+        b, e = block(p.shape[0], comm.rank, comm.size)
+        host = torch.empty((e - b, 3), dtype=torch.float32, pin_memory=True)
+        host.copy_(p[b:e])
+        out = torch.full((e - b,), -1.0, dtype=torch.float32, pin_memory=True)
+        got = PL.unordered_knn(host, comm, E.KnnConfig(k=k), PL.RunInfo(PL.PhaseTimer(False, DEV)), out=out)
+        torch.cuda.synchronize()
+        assert got.data_ptr() == out.data_ptr()
+        return out.clone()
+
+    res = run_loopback(3, fn, DEV)
+    assert torch.equal(torch.cat(res), ref)
