@@ -144,3 +144,19 @@ def test_device_map_and_bootstrap_env():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", ["nccl", "rccl"])
+def test_gpu_app_forced_rccl_matches_cpu(data, backend):
+    """The unordered app on the GPU through its multi-rank path on a forced 1-rank RCCL
+    group (torch.distributed "nccl" or the native communicator "rccl"): same output file
+    as the CPU single-process run."""
+    out = data / f"gpu_{backend}.float"
+    env = dict(ENV, LSKNN_FORCE_DIST="1", LSKNN_DIST_BACKEND=backend, MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port()))
+    p = subprocess.run([sys.executable, "-m", UN, str(data / "pts.float3"), "-o", str(out), "-k", "20",
+                        "--device", "cuda"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert out.read_bytes() == (data / "ref.float").read_bytes()
