@@ -187,7 +187,10 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
     return recv, recv_counts, perm, send_counts
 
 
-STREAM_CHUNK = 1 << 25  # points per host->device chunk of the streamed redistribution
+# points per host->device chunk of the streamed redistribution (env LSKNN_STREAM_CHUNK);
+# smaller chunks shorten the tail after the last copy (forced 1-rank RCCL, 1e8 points:
+# 32M / 16M / 8M -> 170.6 / 169.5 / 169.3 ms per step; profiles/r2_return)
+STREAM_CHUNK = int(os.environ.get("LSKNN_STREAM_CHUNK", str(1 << 24)))
 
 
 @dataclass
