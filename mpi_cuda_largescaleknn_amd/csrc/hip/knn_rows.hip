@@ -258,6 +258,49 @@ __device__ __forceinline__ bool hist_shrink(Lane &s, const uint32_t *pool, int l
 #endif
 }
 
+// Wave min / max of NON-NEGATIVE floats without LDS round trips (LSK_DPP_REDUCE): DPP
+// reductions inside each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_ror:4,
+// row_ror:8), then the four row values combined on the scalar unit (non-negative float
+// bits order as unsigned integers). The generic lsk::wave_min is six dependent
+// ds_bpermute round trips — on the priority-list pop of every node visit.
+#ifndef LSK_DPP_REDUCE
+#define LSK_DPP_REDUCE 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_min_nonneg(float v) {
+#if LSK_DPP_REDUCE
+  v = fminf(v, dpp_f<0xB1>(v));
+  v = fminf(v, dpp_f<0x4E>(v));
+  v = fminf(v, dpp_f<0x124>(v));
+  v = fminf(v, dpp_f<0x128>(v));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 0);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 32);
+  const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 48);
+  return __uint_as_float(min(min(a, b), min(c, d)));
+#else
+  return lsk::wave_min(v);
+#endif
+}
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+#if LSK_DPP_REDUCE
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 0);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 32);
+  const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 48);
+  return __uint_as_float(max(max(a, b), max(c, d)));
+#else
+  return lsk::wave_max(v);
+#endif
+}
+
 // DPP row_newbcast:J — lane J of each 16-lane row to the whole row (folded into the
 // consuming VALU op as a DPP source).
 template <int J>
@@ -668,7 +711,7 @@ __device__ __forceinline__ void flush_pending(Lane &s, WaveCtx &W, const float *
 #if LSK_QPREFILTER
   {
     const float bnd = MODE == MODE_HIST ? hist_bound(s) : (s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f);
-    W.rmax2 = lsk::wave_max(bnd);
+    W.rmax2 = wave_max_nonneg(bnd);
   }
 #endif
   // all loads first (one latency for the batch), then the tests
@@ -984,7 +1027,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
       uint32_t node;
       dfs_mode = sp != 0;
       if (!dfs_mode) {
-        const float m = lsk::wave_min(pqk);
+        const float m = wave_min_nonneg(pqk);
         const int l = (int)__builtin_ctzll(__ballot(pqk == m));
         node = __builtin_amdgcn_readlane(pqn, l);
         if (W.lane == l) pqk = __builtin_inff();
