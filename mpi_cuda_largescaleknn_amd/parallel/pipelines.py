@@ -228,7 +228,13 @@ def redistribute_stream(host_pts: torch.Tensor, comm: Comm, info: RunInfo,
     gpu = dev.type == "cuda"
     size = comm.size
     chunk = max(1, int(chunk or STREAM_CHUNK))
-    spans = [(s, min(s + chunk, n)) for s in range(0, n, chunk)] or [(0, 0)]
+    # every chunk is one all-to-all-v (and one return group member): all ranks must run
+    # the same number of them, so the count is the maximum over ranks and ranks with fewer
+    # points get empty trailing chunks (uneven inputs: prePartitioned files, empty ranks)
+    nch = torch.tensor([max(1, -(-n // chunk))], dtype=torch.int64, device=dev)
+    comm.allreduce_(nch, "max")
+    nch = int(nch.item())
+    spans = [(min(c * chunk, n), min((c + 1) * chunk, n)) for c in range(nch)]
     cur = torch.cuda.current_stream(dev) if gpu else None
     copy_stream = torch.cuda.Stream(dev) if gpu else None
     dchunks, events = [], []

@@ -334,3 +334,22 @@ def test_overlapped_halo_cutoff_caps_bounds(monkeypatch):
         assert torch.equal(out, oracle(p, k, r))
         res[r] = sum(i.counts.get("halo_recv", 0) for i in infos)
     assert res[0.02] < res[math.inf] / 2, res
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("sizes", [(10, 2500, 6000), (0, 4000, 900), (3000, 3000, 2999)])
+def test_streamed_redistribution_uneven_ranks(sizes, monkeypatch):
+    """Ranks with different point counts (and an empty rank) stream different numbers of
+    non-empty chunks: the chunk count is agreed over ranks (trailing empty chunks), so
+    every rank runs the same all-to-all-v sequence; exact results."""
+    monkeypatch.setattr(PL, "FORCE_STREAM", True)
+    monkeypatch.setattr(PL, "STREAM_CHUNK", 1000)
+    n = sum(sizes)
+    p = clustered(n, seed=n)
+    offs = [0, sizes[0], sizes[0] + sizes[1], n]
+    cfg = E.KnnConfig(k=7, publish_levels=4)
+
+    def fn(comm):
+        return PL.unordered_knn(p[offs[comm.rank]:offs[comm.rank + 1]], comm, cfg)
+
+    assert torch.equal(torch.cat(run_loopback(3, fn)), oracle(p, 7))
