@@ -220,3 +220,26 @@ def test_grouped_return_into_pinned_host(groups, monkeypatch):
 
     res = run_loopback(3, fn, DEV)
     assert torch.equal(torch.cat(res), ref)
+
+
+@pytest.mark.parametrize("sizes", [(5, 70_000, 150_000), (0, 90_000, 30_000)])
+def test_streamed_uneven_ranks_gpu(sizes, monkeypatch):
+    """Pinned host inputs of different sizes (one empty): the agreed chunk count gives
+    every rank the same all-to-all-v sequence (empty trailing chunks), grouped return
+    into pinned output included; bit-identical to one rank."""
+    monkeypatch.setattr(PL, "STREAM_CHUNK", 25_000)
+    n = sum(sizes)
+    p = clustered(n, seed=n)
+    offs = [0, sizes[0], sizes[0] + sizes[1], n]
+    ref = single(p, 30)
+
+    def fn(comm):
+        b, e = offs[comm.rank], offs[comm.rank + 1]
+        host = torch.empty((e - b, 3), dtype=torch.float32, pin_memory=True)
+        host.copy_(p[b:e])
+        out = torch.empty(e - b, dtype=torch.float32, pin_memory=True)
+        PL.unordered_knn(host, comm, E.KnnConfig(k=30), out=out)
+        torch.cuda.synchronize()
+        return out.clone()
+
+    assert torch.equal(torch.cat(run_loopback(3, fn, DEV)), ref)
