@@ -179,7 +179,14 @@ class TorchComm(Comm):
         src = send.cpu() if staged else send.contiguous()
         recv = torch.empty((sum(recv_counts), *row_shape), dtype=send.dtype, device=src.device)
         row_bytes = src.element_size() * math.prod(row_shape)
-        if max(send_counts + recv_counts + [0]) * row_bytes <= self.max_msg_bytes:
+        # one collective form on every rank: all_to_all_single when no message of the
+        # exchange exceeds the cap, else the piece rounds. A rank only sees its own rows
+        # and columns of the count matrix, so the largest message is agreed first (a rank
+        # choosing all_to_all_single while a peer posts point-to-point pieces would hang)
+        big = torch.tensor([max(send_counts + recv_counts + [0]) * row_bytes], dtype=torch.int64,
+                           device=self._device if not self.staged else torch.device("cpu"))
+        dist.all_reduce(big, op=dist.ReduceOp.MAX, group=self.group)
+        if int(big.item()) <= self.max_msg_bytes:
             dist.all_to_all_single(recv, src, output_split_sizes=recv_counts,
                                    input_split_sizes=send_counts, group=self.group)
         else:

@@ -89,3 +89,35 @@ def test_alltoallv_and_p2p_in_pieces_gloo(tmp_path):
         assert r[me]["rc"] == [r[src]["counts"][me] for src in range(size)]
         prv = (me - 1) % size
         assert torch.equal(r[me]["got"], torch.arange(1000, dtype=torch.float32) + 1000 * prv)
+
+
+def _mixed_worker(rank, size, port, out_dir):
+    import torch.distributed as dist
+
+    from mpi_cuda_largescaleknn_amd.parallel.comm import TorchComm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    comm = TorchComm("cpu")
+    comm.max_msg_bytes = 4000  # 1000 float32 rows of 1 value
+    # rank 0 sends one big message (3000 rows) to rank 1; every other message is small, so
+    # only ranks 0 and 1 see a message above the cap: all ranks must still pick the same form
+    counts = [[5, 3000, 2], [4, 6, 1], [7, 8, 9]][rank]
+    send = torch.arange(sum(counts), dtype=torch.float32) + 1000 * rank
+    recv, rc = comm.alltoallv(send, counts, recv_counts=[[5, 4, 7], [3000, 6, 8], [2, 1, 9]][rank])
+    torch.save({"recv": recv, "rc": rc}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_alltoallv_form_agreed_across_ranks(tmp_path):
+    """Known receive counts and one message above the cap on a single pair: every rank
+    takes the piece-round form (agreed maximum), no rank waits in all_to_all_single."""
+    mp.spawn(_mixed_worker, args=(3, _port(), str(tmp_path)), nprocs=3, join=True)
+    sends = {r: torch.arange(sum(c), dtype=torch.float32) + 1000 * r
+             for r, c in enumerate([[5, 3000, 2], [4, 6, 1], [7, 8, 9]])}
+    offs = {r: [0, c[0], c[0] + c[1], sum(c)] for r, c in enumerate([[5, 3000, 2], [4, 6, 1], [7, 8, 9]])}
+    for r in range(3):
+        got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        want = torch.cat([sends[j][offs[j][r]:offs[j][r + 1]] for j in range(3)])
+        assert torch.equal(got["recv"], want)
