@@ -584,7 +584,8 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
 
 
 
-FORCE_STREAM = False  # tests: streamed redistribution also for device-resident input
+# tests: streamed redistribution also for device-resident input (env LSKNN_FORCE_STREAM=1)
+FORCE_STREAM = os.environ.get("LSKNN_FORCE_STREAM", "0") == "1"
 
 
 def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,

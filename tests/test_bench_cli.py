@@ -108,3 +108,19 @@ def test_bench_global_set_independent_of_rank_count():
     one = bench.make_points(50000, 0, 1, cpu, "unordered")
     parts = [bench.make_points(50000, r, 3, cpu, "unordered") for r in range(3)]
     assert torch.equal(torch.cat(parts), one)
+
+
+def test_bench_four_ranks_streamed_uneven_chunks():
+    """4 gloo ranks, 30001 points, forced streaming with 7500-point chunks: ranks hold
+    7500 or 7501 points, i.e. one or two chunks — the agreed chunk count keeps their
+    collective sequences equal; all sampled outputs exact."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "4",
+           "--device", "cpu", "--points", "30001", "--k", "12", "--steps", "1", "--warmup", "1"]
+    env = dict(_env(), LSKNN_FORCE_STREAM="1", LSKNN_STREAM_CHUNK="7500")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 4 and rec["config"]["global_batch"] == 30001
+    assert rec["config"]["sampled_exact"] == "256/256"
+    assert sum(rec["detail"]["owned_points_per_rank"]) == 30001
