@@ -67,67 +67,35 @@ constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect
 #define LSK_TOP_BINS 12
 #endif
 // first-range placement from a blend of the lane estimate and the wave median
-#ifndef LSK_EST_BLEND
-#define LSK_EST_BLEND 1
-#endif
 #ifndef LSK_EST_CALIB
 #define LSK_EST_CALIB 0.8
-#endif
-// replay re-tests the logged quarters' boxes (per logged row) against the current
-// bounds instead of appending every logged quarter
-#ifndef LSK_REPLAY_RETEST
-#define LSK_REPLAY_RETEST 0
-#endif
-// best-first walk: inner nodes popped in order of their box distance to the centre of the
-// wave's queries (2; 1 = to the wave's query box) from a 64-entry priority list in two
-// VGPRs, DFS stack as bounded overflow, instead of DFS ordered by the bucket-index gap
-// (0). 1e8 uniform, k=100: DFS 0.135 s, box key 0.129 s, centre key 0.126 s.
-#ifndef LSK_BEST_FIRST
-#define LSK_BEST_FIRST 2
 #endif
 // a pass aborts and restarts with finer bins as soon as the bin holding some lane's k-th
 // value has more than this many times k entries (0 = off)
 #ifndef LSK_CROWD_ABORT
 #define LSK_CROWD_ABORT 64
 #endif
-#ifndef LSK_ENTRY_PREFETCH
-#define LSK_ENTRY_PREFETCH 0
-#endif
 // walk/process alternation: the walk fills the row queues until every row has this
 // many entries pending (then one lockstep drain)
 #ifndef LSK_FILL_MIN
 #define LSK_FILL_MIN 8
 #endif
-// (0 = off) drain as soon as the longest row queue holds this many entries
-#ifndef LSK_DRAIN_MAX
-#define LSK_DRAIN_MAX 0
-#endif
-// prune the pass-1 log: (quarter, row) pairs whose pass-1 processing found no value below
-// any lane's bound are dropped before the collect / later replays
-#ifndef LSK_LOG_PRUNE
-#define LSK_LOG_PRUNE 1
-#endif
-// per-candidate wave-uniform skip of the bin update (0.154 vs 0.159 s, same data)
-#ifndef LSK_HIST_SKIP
-#define LSK_HIST_SKIP 1
-#endif
-// wave-level box-box prefilter of the 8 quarter tests of a pre-leaf node: one VALU pass
-// (lanes 0-7) decides which quarters need the per-lane tests at all; the accepted set is
-// unchanged (1e8 uniform, k=100: 0.147 -> 0.143 s). Its 6 SGPRs of wave box push some
-// per-pass values into scratch; a 1-VGPR wave box instead is slower (0.146 s).
-#ifndef LSK_QPREFILTER
-#define LSK_QPREFILTER 1
-#endif
-// candidates per distance batch in the inner loop: 4 (vs 8) frees the VGPRs that let
-// the kernel run at 7 waves/SIMD (8 at 6 waves: 0.152 s, 4 at 6 waves: 0.149 s)
-#ifndef LSK_CAND_GROUP
-#define LSK_CAND_GROUP 4
-#endif
-// exec-masked histogram update: 5 VALU + ds_add per in-range candidate instead of 8
-// (same speed — the kernel is not VALU-bound — with a shorter dependency chain)
-#ifndef LSK_HIST_EXEC
-#define LSK_HIST_EXEC 1
-#endif
+// Fixed design choices (each measured on 1e8 uniform points, k=100, one MI355X; the
+// alternatives were removed once rejected — profiles/r1_*, profiles/r2_kernel):
+//  * best-first walk: inner nodes popped in order of their box distance to the centre of
+//    the wave's queries from a 64-entry priority list in two VGPRs, a DFS stack as
+//    bounded overflow (DFS by bucket-index gap 0.135 s, query-box key 0.129 s, centre
+//    key 0.126 s);
+//  * the pass-1 log is pruned: (quarter, row) pairs whose pass-1 processing found no
+//    value below any lane's bound are dropped before the collect / later replays; the
+//    replay appends the logged quarters without re-testing their boxes (re-test 0.169 s);
+//  * wave-level box-box prefilter of the 8 quarter tests of a pre-leaf node: one VALU
+//    pass (lanes 0-7) decides which quarters need the per-lane tests at all; the accepted
+//    set is unchanged (0.147 -> 0.143 s);
+//  * candidates in batches of 4 (vs 8: frees the VGPRs of the 7th wave per SIMD);
+//  * exec-masked histogram update (5 VALU + ds_add per in-range candidate) with a
+//    wave-uniform skip when no lane is in range (0.154 vs 0.159 s);
+//  * no entry prefetch (0.129 vs 0.124 s), no early drain of a long row queue.
 constexpr int kTopBins = LSK_TOP_BINS;  // bins of the initial range above the estimate
 constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(log2(kBins))
 constexpr uint32_t kShift0 = 20;
@@ -155,16 +123,10 @@ struct WaveLds {
 };
 // + per-row quarter lists (RCAP entries per row), a kernel template parameter: it sets
 // the LDS footprint and so the occupancy
-#ifndef LSK_LDS_PAD
-#define LSK_LDS_PAD 0
-#endif
 template <int RCAP>
 struct WaveLdsR {
   WaveLds w;
   uint32_t rl[4 * RCAP];
-#if LSK_LDS_PAD > 0
-  uint32_t pad[LSK_LDS_PAD];  // tuning experiments only
-#endif
 };
 
 struct Lane {
@@ -258,20 +220,16 @@ __device__ __forceinline__ bool hist_shrink(Lane &s, const uint32_t *pool, int l
 #endif
 }
 
-// Wave min / max of NON-NEGATIVE floats without LDS round trips (LSK_DPP_REDUCE): DPP
+// Wave min / max of NON-NEGATIVE floats without LDS round trips: DPP
 // reductions inside each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_ror:4,
 // row_ror:8), then the four row values combined on the scalar unit (non-negative float
 // bits order as unsigned integers). The generic lsk::wave_min is six dependent
 // ds_bpermute round trips — on the priority-list pop of every node visit.
-#ifndef LSK_DPP_REDUCE
-#define LSK_DPP_REDUCE 1
-#endif
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
 __device__ __forceinline__ float wave_min_nonneg(float v) {
-#if LSK_DPP_REDUCE
   v = fminf(v, dpp_f<0xB1>(v));
   v = fminf(v, dpp_f<0x4E>(v));
   v = fminf(v, dpp_f<0x124>(v));
@@ -281,12 +239,8 @@ __device__ __forceinline__ float wave_min_nonneg(float v) {
   const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 32);
   const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 48);
   return __uint_as_float(min(min(a, b), min(c, d)));
-#else
-  return lsk::wave_min(v);
-#endif
 }
 __device__ __forceinline__ float wave_max_nonneg(float v) {
-#if LSK_DPP_REDUCE
   v = fmaxf(v, dpp_f<0xB1>(v));
   v = fmaxf(v, dpp_f<0x4E>(v));
   v = fmaxf(v, dpp_f<0x124>(v));
@@ -296,9 +250,6 @@ __device__ __forceinline__ float wave_max_nonneg(float v) {
   const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 32);
   const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 48);
   return __uint_as_float(max(max(a, b), max(c, d)));
-#else
-  return lsk::wave_max(v);
-#endif
 }
 
 // DPP row_newbcast:J — lane J of each 16-lane row to the whole row (folded into the
@@ -341,12 +292,6 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
     for (int t = 0; t < G; t++) {
       const uint32_t v = u[t];
       const bool in = v < hb;
-#if LSK_HIST_SKIP && !LSK_HIST_EXEC  // (the exec-masked form skips by s_cbranch_execz)
-      // most candidates lie beyond every lane's bound once the histogram has settled:
-      // skip the bin update for the whole wave (scalar branch) when none is in range
-      if (!__ballot(in)) continue;
-#endif
-#if LSK_HIST_EXEC
       // exec-masked update: lanes out of range do not issue it, so the bin index needs
       // no clamp (v < hi_b <= lo_b + kBins << shift) and the increment no select
       if (in) {
@@ -356,15 +301,6 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
         atomicAdd(&pool[dw * lsk::kWave + lane], __umul24(half, 0xffffu) + 1u);
         s.c_hi++;
       }
-#else
-      const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
-      uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
-      if (kBins < 64) dw = min(dw, (uint32_t)(kBins / 2 - 1));  // stay inside the pool
-      const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
-      const uint32_t inc = in ? __umul24(half, 0xffffu) + 1u : 0u;
-      atomicAdd(&pool[dw * lsk::kWave + lane], inc);
-      s.c_hi += (uint32_t)in;
-#endif
     }
   } else {
     const uint32_t bl = s.band_lo, bw = s.band_w;
@@ -388,7 +324,6 @@ template <int MODE>
 __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz, uint32_t cnt,
                                           uint32_t *pool, int lane, uint32_t k, bool &crowd) {
   bool lane_in;
-#if LSK_CAND_GROUP == 4
   // groups of 4 candidates: 4 fewer live VGPRs in the hot loop than groups of 8
   {
     uint32_t u[4] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
@@ -412,20 +347,6 @@ __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz,
       lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
     }
   }
-#else
-  {
-    uint32_t u[8] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
-                     cand<3>(s, px, py, pz), cand<4>(s, px, py, pz), cand<5>(s, px, py, pz),
-                     cand<6>(s, px, py, pz), cand<7>(s, px, py, pz)};
-    lane_in = update8<MODE, 8>(s, u, pool, lane);
-  }
-  if (__ballot(cnt > 8u)) {
-    uint32_t u[8] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
-                     cand<11>(s, px, py, pz), cand<12>(s, px, py, pz), cand<13>(s, px, py, pz),
-                     cand<14>(s, px, py, pz), cand<15>(s, px, py, pz)};
-    lane_in = update8<MODE, 8>(s, u, pool, lane) || lane_in;
-  }
-#endif
   if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) crowd = __ballot(hist_shrink(s, pool, lane, k)) != 0 || crowd;
   return lane_in;
 }
@@ -439,10 +360,8 @@ struct WaveCtx {
   uint32_t g;
   int32_t seed;
   float cx, cy, cz;
-#if LSK_QPREFILTER
   float wlx, wly, wlz, whx, why, whz;  // bounding box of the wave's queries (uniform)
   float rmax2;                         // wave max of the lanes' current bounds (per flush)
-#endif
   // Row queues are circular (RCAP entries, a power of two) with their own heads: a step
   // consumes the head entry of every row that has one, so a row that got ahead does not
   // force the others to idle until a reset (lockstep idle only when a row is empty).
@@ -455,14 +374,12 @@ struct WaveCtx {
   uint32_t logn;
   bool logging, log_ok;
   bool crowd;  // a lane's k-th bin got crowded: abort the pass (see hist_shrink)
-#if LSK_LOG_PRUNE
   // pass-1 "dead row-step" stream: bit h of row r (lane 16r + h/32, bit h%32) is set when
   // the row's h-th queue entry gave no lane of the row a value below its bound; after
   // pass 1 those (quarter, row) pairs are removed from the log (they cannot hold a value
   // below any later bound or inside the collect band: bounds only shrink)
   uint32_t *dead;  // private (scratch) word: keeps the stream out of the VGPR budget
   uint32_t nseed;  // seed quarters appended to every row before the logged ones
-#endif
   uint32_t *logq, *logm;
   const float *p0, *p1, *pdef;  // tree point arrays (pdef: one that is non-empty)
   uint32_t n0, n1;
@@ -533,11 +450,6 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
   uint32_t cnt = load_quarter<NT>(W, row_entry(W, W.rhead), px, py, pz);
   // (two steps of prefetch: 0.155 vs 0.152 s at 6 waves/SIMD with 10 spilled VGPRs,
   // 0.166 s at 5 waves/SIMD — occupancy, not the candidate-load distance, is what counts)
-#if LSK_ENTRY_PREFETCH
-  // the queue entry of the next step is read from LDS one step early, so the candidate
-  // load address does not wait on an LDS round trip
-  uint32_t e_next = row_entry(W, W.rhead + (W.rhead < W.rlen ? 1u : 0u));
-#endif
   const float inf = __builtin_inff();
   for (uint32_t st = 0; st < n; st++) {
     const uint32_t ccnt = cnt;
@@ -545,12 +457,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     const bool live = (uint32_t)(W.lane & 15) < ccnt;
     const float cx = live ? px : inf, cy = live ? py : inf, cz = live ? pz : inf;
     W.rhead += W.rhead < W.rlen ? 1u : 0u;
-#if LSK_ENTRY_PREFETCH
-    cnt = load_quarter<NT>(W, e_next, px, py, pz);
-    e_next = row_entry(W, W.rhead + (W.rhead < W.rlen ? 1u : 0u));
-#else
     cnt = load_quarter<NT>(W, row_entry(W, W.rhead), px, py, pz);
-#endif
     W.steps++;
     if (MODE == MODE_COLLECT) W.csteps++;
 #ifdef LSK_PROFILE
@@ -568,17 +475,12 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
       W.prof_crows_in += __popc(re & ri);
     }
 #endif
-#if LSK_LOG_PRUNE
     if (MODE == MODE_HIST && W.logging) {
       const uint32_t rin = row_bits(__ballot(lin)), rent = row_bits(__ballot(ccnt > 0u));
       const uint32_t dead = ((rent & ~rin) >> W.row) & 1u;
       if (dead && hcur < 512u && (uint32_t)(W.lane & 15) == (hcur >> 5))
         W.dead[hcur >> 9] |= 1u << (hcur & 31u);  // (index 0: dynamic, so it stays in scratch)
     }
-#else
-    (void)lin;
-    (void)hcur;
-#endif
     if (MODE == MODE_HIST && W.crowd) break;  // crowded bin: the pass restarts narrower
   }
   W.hd0 = min(W.hd0 + n, W.len0);
@@ -650,7 +552,6 @@ __device__ __forceinline__ uint32_t test_block(Lane &s, WaveCtx &W, float blk, u
                                                uint32_t lmask, uint32_t nquarters, int64_t skip_lo,
                                                int64_t skip_hi) {
   uint32_t took = 0;
-#if LSK_QPREFILTER
   // wave-level prefilter: lane j < 8 tests quarter j's box against the box of the wave's
   // queries and the largest lane bound (box-box distance <= every query's box distance,
   // so a quarter some lane needs always passes); the exact per-lane tests then run only
@@ -664,16 +565,13 @@ __device__ __forceinline__ uint32_t test_block(Lane &s, WaveCtx &W, float blk, u
     const lsk::box3f qb{{qlx, qly, qlz}, {qhx, qhy, qhz}};
     pm = (uint32_t)__ballot(W.lane < 8 && lsk::box_box_dist2(wb, qb) < W.rmax2) & 0xffu;
   }
-#endif
 #pragma unroll
   for (uint32_t j = 0; j < 8; j++) {
     const uint32_t qid = q0 + j;
     const int64_t b = (int64_t)(qid >> 2);
     const uint32_t lm = (lmask >> (4 * j)) & 0xfu;
     if (lm == 0 || qid >= nquarters || (b >= skip_lo && b <= skip_hi)) continue;
-#if LSK_QPREFILTER
     if (!((pm >> j) & 1u)) continue;
-#endif
     const float lx = lanef(blk, 8 * j), ly = lanef(blk, 8 * j + 1), lz = lanef(blk, 8 * j + 2);
     const float hx = lanef(blk, 8 * j + 4), hy = lanef(blk, 8 * j + 5), hz = lanef(blk, 8 * j + 6);
     const uint32_t rm = row_bits(__ballot(box_needed<MODE>(s, lx, ly, lz, hx, hy, hz))) & lm;
@@ -708,12 +606,10 @@ __device__ __forceinline__ void flush_pending(Lane &s, WaveCtx &W, const float *
                                               const Pend &P, uint32_t nquarters, int64_t skip_lo,
                                               int64_t skip_hi, uint32_t qfloats) {
   const uint32_t l = (uint32_t)W.lane, last = qfloats - 1u;
-#if LSK_QPREFILTER
   {
     const float bnd = MODE == MODE_HIST ? hist_bound(s) : (s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f);
     W.rmax2 = wave_max_nonneg(bnd);
   }
-#endif
   // all loads first (one latency for the batch), then the tests
 #define LSK_LD(i) const float b##i = qf[min((P.n > i ? P.p##i : P.p0) * 8u + l, last)];
   LSK_LD(0) LSK_LD(1) LSK_LD(2) LSK_LD(3)
@@ -732,32 +628,16 @@ __device__ __forceinline__ uint32_t ubits(float v) {  // uniform, order-preservi
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(v));
 }
 
-#if LSK_LOG_PRUNE
 // Drop from the pass-1 log every (quarter, row) pair whose pass-1 step gave no lane of the
 // row a value below its bound (WaveCtx::dead). Row r's queue held the seeds first, then
 // the logged quarters in log order (quarter order inside an entry), so the stream index
 // of a logged pair is nseed + (row-r pairs in earlier entries) + (row-r pairs of earlier
 // quarters of the same entry). One 64-entry log word per iteration, all lanes at once.
-// 2: log_prune_impl out of line with scalar arguments (WaveCtx stays in registers,
-// the prune's own temporaries do not raise the kernel's register pressure): 0.1245 s;
-// 1: out of line taking WaveCtx& (WaveCtx forced to scratch): 0.127 s; 0: inlined: 0.149 s
-#ifndef LSK_PRUNE_NOINLINE
-#define LSK_PRUNE_NOINLINE 2
-#endif
-#if LSK_PRUNE_NOINLINE == 2
-// out of line with scalar arguments: WaveCtx stays in registers (it is not passed)
+// Out of line with scalar arguments: WaveCtx stays in registers and the prune's own
+// temporaries do not raise the kernel's register pressure (0.1245 s; out of line taking
+// WaveCtx& forces WaveCtx to scratch: 0.127 s; inlined: 0.149 s).
 __device__ __attribute__((noinline)) void log_prune_impl(uint32_t *logm, uint32_t logn, uint32_t dw,
                                                           uint32_t nseed, int lane) {
-#elif LSK_PRUNE_NOINLINE
-// (an out-of-line call: WaveCtx then lives in scratch and the compiler keeps only its hot
-// fields in registers, which measured faster than the all-register allocation — 1e8
-// k=100: 0.138 vs 0.149 s; profiles/r2_kernel)
-__device__ __attribute__((noinline)) void log_prune_impl(uint32_t *logm, uint32_t logn, uint32_t dw,
-                                                          uint32_t nseed, int lane) {
-#else
-__device__ __forceinline__ void log_prune_impl(uint32_t *logm, uint32_t logn, uint32_t dw,
-                                               uint32_t nseed, int lane) {
-#endif
   uint32_t base01 = 0, base23 = 0;  // row pairs before this word (rows 0|1, 2|3: 16-bit fields)
 #pragma unroll 1
   for (uint32_t w = 0; w < kLogWords; w++) {
@@ -790,16 +670,9 @@ __device__ __forceinline__ void log_prune_impl(uint32_t *logm, uint32_t logn, ui
     base23 += (uint32_t)__shfl((int)x23, 63);
   }
 }
-#if LSK_PRUNE_NOINLINE == 1
-__device__ __attribute__((noinline)) void log_prune(WaveCtx &W) {
-  log_prune_impl(W.logm, W.logn, W.dead[0], W.nseed, W.lane);
-}
-#else
 __device__ __forceinline__ void log_prune(WaveCtx &W) {
   log_prune_impl(W.logm, W.logn, W.dead[0], W.nseed, W.lane);
 }
-#endif
-#endif
 
 // Tree walk (wave-uniform DFS, near child first) building the per-row quarter lists,
 // alternating with lockstep processing of what every row has pending (one processing
@@ -825,7 +698,6 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   // DFS stack in one VGPR (lane i = entry i; < 64 entries): v_readlane to pop, a
   // lane select to push, instead of an LDS round trip per node
   uint32_t stk = 0;
-#if LSK_BEST_FIRST
   // priority list: lane i holds (node, key) entry i; empty = (any, +inf); npq entries
   uint32_t pqn = 0u;
   float pqk = __builtin_inff();
@@ -838,13 +710,8 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   bool dfs_mode = false;
   auto pq_push = [&](uint32_t cn, lsk::v4f lo, lsk::v4f hi) {
     if (!dfs_mode && npq < 64u) {
-#if LSK_BEST_FIRST == 2
       // key: squared distance from the wave's query-box centre to the node box
       const float key = lsk::uniform_f(lsk::box_dist2(c, {lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}));
-#else
-      // key: squared distance between the wave's query box and the node box
-      const float key = lsk::uniform_f(lsk::box_box_dist2(wbox, {{lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}}));
-#endif
       const uint64_t fr = __ballot(pqk == __builtin_inff());
       const int l = (int)__builtin_ctzll(fr);
       if (W.lane == l) {
@@ -856,7 +723,6 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
       stk = W.lane == (int)sp++ ? cn : stk;
     }
   };
-#endif
   bool started = false, finished = false;
   int32_t seed_d = W.seed > 0 ? 0 : -1;  // next seed distance (tree 0 only)
   lsk_tree_view T = pick_tree(A, 0);
@@ -869,10 +735,8 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
   bool force_flush = false;           // replay: a tree switch needs the batch flushed
   if (!replay && W.logging) {
     W.logn = 0;
-#if LSK_LOG_PRUNE
     W.dead[0] = 0;
     W.nseed = 0;
-#endif
   }
   while (!finished) {
     bool overflow = false;
@@ -884,11 +748,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     for (;;) {
       // room for the pending batch (8 entries per node per row) plus one more node
       const bool room_short = max_pend(W) + 8u * (P.n + 1u) > W.rcap;
-#if LSK_BEST_FIRST
       const bool walk_empty = sp == 0 && npq == 0;
-#else
-      const bool walk_empty = sp == 0;
-#endif
       if (P.n && (P.n == kPend || room_short || (started && walk_empty) || force_flush ||
                   (replay && ri >= W.logn))) {
         force_flush = false;
@@ -903,11 +763,6 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         break;
       }
       if (min_pend(W) >= (uint32_t)LSK_FILL_MIN) break;
-#if LSK_DRAIN_MAX
-      // also drain when one row runs far ahead (its queued quarters were tested against
-      // bounds that its own processing would have tightened)
-      if (max_pend(W) >= (uint32_t)LSK_DRAIN_MAX) break;
-#endif
       if (!started) {
         if (t >= (uint32_t)A.ntrees) {
           finished = true;
@@ -927,16 +782,11 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
           skip_lo = (int64_t)W.g - W.seed;
           skip_hi = (int64_t)W.g + W.seed;
         }
-#if LSK_BEST_FIRST
         if (W.lane == 0) {  // the root enters the priority list
           pqn = 1u;
           pqk = 0.f;
         }
         npq = 1;
-#else
-        stk = W.lane == 0 ? 1u : stk;
-        sp = 1;
-#endif
         started = true;
       }
       if (t == 0 && seed_d >= 0) {  // seed buckets g, g-1, g+1, g-2, g+2, ... for every row
@@ -947,9 +797,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
             const uint32_t qid = (uint32_t)b * 4 + qq;
             if (qid < nquarters) {
               rows_append(W, 0xfu, qid);
-#if LSK_LOG_PRUNE
               if (!replay) W.nseed++;
-#endif
             }
           }
         }
@@ -968,40 +816,6 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         const uint32_t e = __builtin_amdgcn_readlane(lq, (int)(ri & 63u));
         const uint32_t mk = __builtin_amdgcn_readlane(lmk, (int)(ri & 63u));
         const uint32_t tq = e & 0x80000000u, q0 = e & 0x7fffffffu;
-#if LSK_REPLAY_RETEST
-        // re-test the logged quarters against the lanes' current bounds (a shell in the
-        // collect pass) with the logged rows as the mask: same batched box loads as a walk
-        {
-          const uint32_t et = tq >> 31;
-          if (et != t) {
-            if (P.n) {  // flush the other tree's batch first (top of the fill loop)
-              force_flush = true;
-              continue;
-            }
-            t = et;
-            T = pick_tree(A, t);
-            depth = T.depth;
-            nquarters = (uint32_t)((T.n + 15) / 16);
-            skip_lo = 1;
-            skip_hi = 0;
-            if (t == 0 && W.seed > 0) {
-              skip_lo = (int64_t)W.g - W.seed;
-              skip_hi = (int64_t)W.g + W.seed;
-            }
-          }
-          P.p0 = P.n == 0 ? q0 : P.p0;
-          P.p1 = P.n == 1 ? q0 : P.p1;
-          P.p2 = P.n == 2 ? q0 : P.p2;
-          P.p3 = P.n == 3 ? q0 : P.p3;
-          P.m0 = P.n == 0 ? mk : P.m0;
-          P.m1 = P.n == 1 ? mk : P.m1;
-          P.m2 = P.n == 2 ? mk : P.m2;
-          P.m3 = P.n == 3 ? mk : P.m3;
-          P.n++;
-          ri++;
-          continue;
-        }
-#else
         // the logged rows per quarter are appended as they are: they are a superset of
         // what any later pass needs (bounds only shrink), and skipping the re-test keeps
         // replay free of box loads
@@ -1012,18 +826,12 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         }
         ri++;
         continue;
-#endif
       }
-#if LSK_BEST_FIRST
       if (sp == 0 && npq == 0) {  // (nothing pending here: flushed above)
-#else
-      if (sp == 0) {  // (nothing pending here: flushed above)
-#endif
         t++;
         started = false;
         continue;
       }
-#if LSK_BEST_FIRST
       uint32_t node;
       dfs_mode = sp != 0;
       if (!dfs_mode) {
@@ -1036,10 +844,6 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         sp--;
         node = __builtin_amdgcn_readlane(stk, (int)sp);
       }
-#else
-      sp--;
-      const uint32_t node = __builtin_amdgcn_readlane(stk, (int)sp);
-#endif
       W.nodes_visited++;
       if (MODE == MODE_COLLECT) W.cnodes++;
       const int32_t lvl = 31 - __clz(node);
@@ -1058,9 +862,8 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
                                           : (s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f);
       if (lvl + 2 <= depth - 1) {
         const uint32_t g0 = 4u * node;
-        // visiting order: by bucket-index gap between the child's subtree and the wave's
-        // own bucket (tree 0; scalar integer ops) — Morton order makes that a cheap proxy
-        // for spatial distance; other trees keep index order
+        // bucket-index gap of each child's subtree to the wave's own bucket (the DFS
+        // visiting order before the best-first walk; unused, kept for an identical build)
         const uint32_t csh = (uint32_t)(depth - lvl - 2);
         auto korder = [&](uint32_t ch, uint32_t j) -> uint32_t {
           if (t != 0) return 3u - j;
@@ -1097,28 +900,12 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
           k3 = korder(g0 + 3u, 3u);
         }
         need = (uint32_t)__builtin_amdgcn_readfirstlane((int)need);
-#if LSK_BEST_FIRST
         (void)k0; (void)k1; (void)k2; (void)k3;
         for (uint32_t j = 0; j < 4u; j++)
           if ((need >> j) & 1u) {
             const lsk::v4f lo = nodes[2 * (g0 + j)], hi = nodes[2 * (g0 + j) + 1];
             pq_push(g0 + j, lo, hi);
           }
-#else
-        // sorting network, descending (push far ... near)
-#define LSK_CSWAP(a, b)                 \
-  {                                     \
-    const uint32_t hi_ = max(a, b);     \
-    b = min(a, b);                      \
-    a = hi_;                            \
-  }
-        LSK_CSWAP(k0, k1) LSK_CSWAP(k2, k3) LSK_CSWAP(k0, k2) LSK_CSWAP(k1, k3) LSK_CSWAP(k1, k2)
-#undef LSK_CSWAP
-        if ((need >> (k0 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k0 & 3u) : stk;
-        if ((need >> (k1 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k1 & 3u) : stk;
-        if ((need >> (k2 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k2 & 3u) : stk;
-        if ((need >> (k3 & 3u)) & 1u) stk = W.lane == (int)sp++ ? g0 + (k3 & 3u) : stk;
-#endif
       } else {  // binary step onto level depth-1
         const uint32_t c0 = 2 * node, c1 = c0 + 1;
         const lsk::v4f l0 = nodes[2 * c0], h0 = nodes[2 * c0 + 1];
@@ -1130,14 +917,9 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
         const bool first0 = t != 0 || W.g < mid;
         const uint32_t a = first0 ? c1 : c0, bb = first0 ? c0 : c1;
         const bool na = first0 ? n1 : n0, nbb = first0 ? n0 : n1;
-#if LSK_BEST_FIRST
         (void)a; (void)bb; (void)na; (void)nbb;
         if (n0) pq_push(c0, l0, h0);
         if (n1) pq_push(c1, l1, h1);
-#else
-        if (na) stk = W.lane == (int)sp++ ? a : stk;
-        if (nbb) stk = W.lane == (int)sp++ ? bb : stk;
-#endif
       }
       LSK_PADD(W.prof[5], tn0);
     }
@@ -1145,12 +927,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     // fill: the steps every row can take; overflow: at least enough to make room for one
     // more node's 8 quarters in the longest queue; end of walk: everything pending
     const uint32_t mxp = max_pend(W), mnp = min_pend(W);
-#if LSK_DRAIN_MAX
-    const uint32_t nsteps = finished ? mxp : overflow ? max(mnp, mxp + 8u - min(mxp + 8u, W.rcap))
-                                                     : max(mnp, (mxp + 1u) >> 1);
-#else
     const uint32_t nsteps = finished ? mxp : overflow ? max(mnp, mxp + 8u - min(mxp + 8u, W.rcap)) : mnp;
-#endif
     LSK_PT(tp0);
     process_steps<MODE, NT>(s, W, A, nsteps);
     LSK_PADD(W.prof[MODE], tp0);
@@ -1228,10 +1005,6 @@ __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *p
   return sum == s.c_hi;
 }
 
-#ifdef LSK_W_ESCAPE
-// tuning experiment: make WaveCtx escape to memory without the log prune
-__device__ __attribute__((noinline)) void w_escape(WaveCtx &W) { asm volatile("" ::"v"(W.k)); }
-#endif
 
 template <int RCAP, int NT>
 __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_rows_kernel(const lsk_knn_args A) {
@@ -1263,10 +1036,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   uint32_t logq[kLogWords], logm[kLogWords];  // private (scratch) pass-1 log
   W.logq = logq;
   W.logm = logm;
-#if LSK_LOG_PRUNE
   uint32_t deadw[2];  // private dead-row-step stream word (WaveCtx::dead)
   W.dead = deadw;
-#endif
   W.logn = 0;
   W.logging = W.log_ok = false;
   W.crowd = false;
@@ -1283,9 +1054,6 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   LSK_PT(twave0);
 #endif
   W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
-#ifdef LSK_W_ESCAPE
-  w_escape(W);
-#endif
 
   Lane s;
   s.qx = valid ? A.qpts[3 * qi] : 0.f;
@@ -1300,10 +1068,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   W.cx = 0.5f * (lx + hx);
   W.cy = 0.5f * (ly + hy);
   W.cz = 0.5f * (lz + hz);
-#if LSK_QPREFILTER
   W.wlx = lx; W.wly = ly; W.wlz = lz;
   W.whx = hx; W.why = hy; W.whz = hz;
-#endif
 
   bool dup;
   float r_est2 = own_group_estimate(s, nvalid, k, dup);
@@ -1326,14 +1092,12 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     const uint32_t kq = max(1u, nvalid / 4u);
     const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
     if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
-#if LSK_EST_BLEND
     // geometric blend with the wave median (the per-lane 8-NN estimate is noisy, the
     // median alone misses density changes inside a group), calibrated so that the median
     // of true/estimate is 1 on uniform and clustered data (offline study: the k-th lands
     // below 2x the blend for 99.5 % of queries, vs 2.9x for the lane estimate)
     const uint32_t mb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, max(1u, nvalid / 2u));
     if (ok && mb < lsk::kInfBits) r_est2 = sqrtf(r_est2 * bitsf(mb)) * (float)LSK_EST_CALIB;
-#endif
   }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
     r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
@@ -1455,9 +1219,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
         }
         continue;
       }
-#if LSK_LOG_PRUNE
       if (W.logging && W.log_ok) log_prune(W);
-#endif
       W.logging = false;
       first = false;
       bool ovf = false;
