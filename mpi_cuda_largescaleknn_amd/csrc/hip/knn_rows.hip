@@ -46,10 +46,10 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #endif
 #ifndef LSK_ROWS_MINW
 // 7 waves/SIMD: 40 bins keep the LDS at 22 KB/block (7 blocks/CU) and the allocator fits
-// 72 VGPRs with 4-candidate batches (its 10 spills sit in per-pass code, not in the
-// inner loops). Occupancy is what this latency-bound kernel runs on (1e8 pts, k=100):
-// 5 waves 0.166 s, 6 waves 0.149-0.152 s, 7 waves 0.147 s, 8 waves (36 bins, 24 spills)
-// 0.155 s.
+// 72 VGPRs with 4-candidate batches (its spills sit in per-pass code, not in the inner
+// loops). 1e8 pts, k=100 (round 1): 5 waves 0.166 s, 6 waves 0.149-0.152 s, 7 waves
+// 0.147 s, 8 waves (36 bins) 0.155 s; round 2: 8 waves 0.137 vs 7 waves 0.126 s. The
+// final kernel is VALU-issue bound (VALUBusy 74 %, profiles/r2_pmc_final).
 #define LSK_ROWS_MINW 7
 #endif
 // 40 bins of 1/8 octave of d² (kShift0) around the estimate (48 bins: 0.150 s at 6
