@@ -151,9 +151,10 @@ def main():
     def _step(phases: bool = args.phases):
         nonlocal info_last
         info = PL.RunInfo(PL.PhaseTimer(phases, device))
-        if comm.distributed and args.variant == "unordered" and args.mode == "halo":
-            # several ranks: the redistribution streams the host points to the device in
-            # chunks overlapped with the all-to-all (pipelines.redistribute_stream)
+        if args.variant == "unordered" and args.mode == "halo":
+            # the pipeline streams the host points to the device in chunks: on several
+            # ranks overlapped with the all-to-all (pipelines.redistribute_stream), on one
+            # with the per-chunk bounds and curve keys (pipelines.upload_keyed)
             pts = host_pts
         else:
             pts = host_pts.to(device, non_blocking=True)

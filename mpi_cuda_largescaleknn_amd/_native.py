@@ -137,6 +137,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_box_finalize": ([vp, vp], i32),
         "lsk_hip_radius_hint": ([vp, i64, i32, vp, vp], i32),
         "lsk_hip_morton": ([vp, i64, vp, vp, vp, i32, vp], i32),
+        "lsk_hip_morton_ex": ([vp, i64, vp, vp, vp, i32, i64, vp, vp], i32),
         "lsk_hip_gather3": ([vp, vp, i64, vp, vp], i32),
         "lsk_hip_scatter1": ([vp, vp, i64, vp, i32, vp], i32),
         "lsk_hip_finalize": ([vp, i64, vp, vp], i32),

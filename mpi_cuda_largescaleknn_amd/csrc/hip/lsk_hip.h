@@ -39,6 +39,9 @@ int lsk_hip_box_finalize(float *box, void *stream);
 // 0 = Morton, 1 = Hilbert, common.h); vals[i] = i (if vals is not null).
 int lsk_hip_morton(const float *pts, int64_t n, const float *box, uint32_t *keys,
                    uint32_t *vals, int curve, void *stream);
+// same with vals[i] = base + i and an optional device flag (nothing happens if *flag == 0)
+int lsk_hip_morton_ex(const float *pts, int64_t n, const float *box, uint32_t *keys, uint32_t *vals, int curve,
+                      int64_t base, const int *flag, void *stream);
 // dst[i] = src[idx[i]] (float3 gather).
 int lsk_hip_gather3(const float *src, const uint32_t *idx, int64_t n, float *dst, void *stream);
 // dst[idx[i]] = src[i] (float scatter), optional sqrt-finalisation.

@@ -120,10 +120,15 @@ __global__ void radius_hint_kernel(const float *box, int64_t n_total, int32_t k,
   out[0] = r2;
 }
 
+// keys (and vals = base + i) of pts in the cube of `box`; with `flag` the kernel does
+// nothing unless *flag != 0 (a device-side decision inside a captured step: the
+// streamed single-rank upload re-keys only when a point fell outside its provisional box)
 __global__ __launch_bounds__(256) void morton_kernel(const float *__restrict__ pts, int64_t n,
                                                      const float *__restrict__ box,
                                                      uint32_t *__restrict__ keys,
-                                                     uint32_t *__restrict__ vals, int curve) {
+                                                     uint32_t *__restrict__ vals, int curve,
+                                                     uint32_t base, const int *__restrict__ flag) {
+  if (flag && *flag == 0) return;
   const float ox = box[0], oy = box[1], oz = box[2], s = box[6];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -131,7 +136,7 @@ __global__ __launch_bounds__(256) void morton_kernel(const float *__restrict__ p
     const uint32_t iy = lsk::morton_quant(pts[3 * i + 1], oy, s);
     const uint32_t iz = lsk::morton_quant(pts[3 * i + 2], oz, s);
     keys[i] = lsk::curve3(curve, ix, iy, iz);
-    if (vals) vals[i] = (uint32_t)i;
+    if (vals) vals[i] = base + (uint32_t)i;
   }
 }
 
@@ -280,8 +285,22 @@ extern "C" int lsk_hip_morton(const float *pts, int64_t n, const float *box, uin
                               uint32_t *vals, int curve, void *stream) {
   if (n <= 0) return 0;
   morton_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(pts, n, box,
-                                                                             keys, vals, curve);
+                                                                             keys, vals, curve, 0u,
+                                                                             nullptr);
   LSK_CHECK_LAUNCH("morton");
+  return 0;
+}
+
+extern "C" int lsk_hip_morton_ex(const float *pts, int64_t n, const float *box, uint32_t *keys,
+                                 uint32_t *vals, int curve, int64_t base, const int *flag, void *stream) {
+  if (n <= 0) return 0;
+  if (base < 0 || base + n > ((int64_t)1 << 32)) {
+    lsk::set_last_error("morton_ex: indices must fit in 32 bits");
+    return 1;
+  }
+  morton_kernel<<<lsk_blocks(n, 256 * 4, 8192), 256, 0, (hipStream_t)stream>>>(
+      pts, n, box, keys, vals, curve, (uint32_t)base, flag);
+  LSK_CHECK_LAUNCH("morton_ex");
   return 0;
 }
 

@@ -88,14 +88,16 @@ class KnnStats:
         self.counters["fallback_queries"] = self.counters.get("fallback_queries", 0) + int(n)
 
 
-def build_index(points: torch.Tensor, box: torch.Tensor | None = None) -> LocalIndex:
-    """Sort points along the Morton curve of `box` (default: their own bounds) and
-    build the bucket tree."""
+def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
+                keys: tuple | None = None) -> LocalIndex:
+    """Sort points along the space-filling curve of `box` (default: their own bounds) and
+    build the bucket tree. `keys` = (keys, iota) computed already (the streamed upload
+    keys each chunk as it lands)."""
     points = points.contiguous()
     n = points.shape[0]
     if box is None:
         box = K.bounds(points)
-    keys, iota = K.morton(points, box)
+    keys, iota = keys if keys is not None else K.morton(points, box)
     skeys, perm = K.sort_pairs(keys, iota, 30)
     perm = refine_heavy_cells(points, skeys, perm)
     pts = K.gather3(points, perm, pad=K.PAD_POINTS)

@@ -95,6 +95,16 @@ def morton(pts: torch.Tensor, box: torch.Tensor, with_iota: bool = True, curve: 
     return keys, vals
 
 
+def morton_into(pts: torch.Tensor, box: torch.Tensor, keys: torch.Tensor, vals: torch.Tensor | None,
+                base: int, flag: torch.Tensor | None = None, curve: str | None = None) -> None:
+    """GPU: keys of pts (and vals = base + i) written into the given (slice) tensors; with
+    a device int32 `flag` nothing is written unless flag != 0 (decided on the device)."""
+    check(_native.hip().lsk_hip_morton_ex(_ptr(pts), pts.shape[0], _ptr(box), _ptr(keys),
+                                          _ptr(vals) if vals is not None else None, CURVES[curve or CURVE],
+                                          int(base), _ptr(flag) if flag is not None else None,
+                                          _stream(pts)), "morton_ex")
+
+
 def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, key_bits: int = 30):
     """Stable sort of (key, value) int32 pairs by the low `key_bits` bits of key (unsigned)."""
     n = keys.shape[0]
