@@ -36,5 +36,7 @@ for rep in range(2):
     print(f"loopback x{P} {n}: {time.perf_counter() - t:.3f}s", flush=True)
 for r, (_, info) in enumerate(res):
     print(r, {k: round(v, 4) for k, v in info.timer.times.items()}, info.counts, flush=True)
+    if cfg.collect_stats:
+        print("   stats", {k: v for k, v in info.stats.counters.items() if v}, flush=True)
 single = E.knn_distances(p, 100)
 print("equal to single:", torch.equal(torch.cat([o for o, _ in res]), single))
