@@ -5,8 +5,10 @@
 * ``lib/liblsknn_hip.so``   — hand-written gfx950 HIP kernels, built with
   ``hipcc --offload-arch=gfx950`` (cross-compiles without a GPU).
 * ``lib/liblsknn_comm.so``  — native RCCL communicator (host code, RCCL dlopen'ed).
+* ``lib/liblsknn_mpi.so``   — native MPI host communicator (g++ against the image's
+  MPICH; skipped when no MPI installation is found).
 
-Both are rebuilt only when a source or header is newer than the library. The
+All are rebuilt only when a source or header is newer than the library. The
 libraries are git-ignored but travel to the GPU box with the working tree.
 """
 from __future__ import annotations
@@ -129,8 +131,42 @@ def build_comm(force: bool = False, verbose: bool = False) -> str:
     return COMM_LIB
 
 
+MPI_LIB = os.path.join(LIB_DIR, "liblsknn_mpi.so")
+
+
+def mpi_home() -> str | None:
+    """MPI installation with include/mpi.h and lib/libmpi.so: LSKNN_MPI_HOME, else the
+    image's MPICH (/opt/conda); None when there is none (the MPI backend is optional)."""
+    for home in (os.environ.get("LSKNN_MPI_HOME"), "/opt/conda"):
+        if home and os.path.exists(os.path.join(home, "include", "mpi.h")) and \
+                os.path.exists(os.path.join(home, "lib", "libmpi.so")):
+            return home
+    return None
+
+
+def build_mpi(force: bool = False, verbose: bool = False) -> str | None:
+    """Native MPI host communicator (csrc/mpi): plain C++ linked against the MPI library
+    (rpath to it), loaded only when LSKNN_DIST_BACKEND=mpi."""
+    home = mpi_home()
+    if home is None:
+        return None
+    srcs = _sources("mpi", "cpp")
+    if force or _stale(MPI_LIB, srcs):
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = MPI_LIB + ".tmp"
+        lib = os.path.join(home, "lib")
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{os.path.join(home, 'include')}",
+               "-o", tmp, *srcs, f"-L{lib}", f"-Wl,-rpath,{lib}", "-lmpi"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        _run(cmd)
+        os.replace(tmp, MPI_LIB)
+    return MPI_LIB
+
+
 def build_all(force: bool = False, verbose: bool = False) -> tuple[str, str]:
     build_comm(force, verbose)
+    build_mpi(force, verbose)
     return build_host(force, verbose), build_hip(force, verbose)
 
 

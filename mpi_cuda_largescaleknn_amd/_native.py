@@ -240,6 +240,33 @@ def comm() -> C.CDLL:
     return _comm_lib
 
 
+_mpi_lib = None
+
+
+def mpi() -> C.CDLL:
+    """The native MPI host communicator library (csrc/mpi/mpi_comm.cpp)."""
+    global _mpi_lib
+    if _mpi_lib is None:
+        with _lock:
+            if _mpi_lib is None:
+                path = _build.build_mpi()
+                if path is None:
+                    raise NativeError("LSKNN_DIST_BACKEND=mpi: no MPI installation found "
+                                      "(set LSKNN_MPI_HOME to a directory with include/mpi.h and lib/libmpi.so)")
+                lib = C.CDLL(path)
+                lib.lsk_mpi_last_error.restype = C.c_char_p
+                lib.lsk_mpi_init.argtypes = [C.POINTER(C.c_int), C.POINTER(C.c_int)]
+                lib.lsk_mpi_abort.argtypes = [i32]
+                lib.lsk_mpi_abort.restype = None
+                lib.lsk_mpi_bcast.argtypes = [vp, i64, i32]
+                lib.lsk_mpi_allreduce.argtypes = [vp, i64, i32, i32]
+                lib.lsk_mpi_allgather.argtypes = [vp, vp, i64, i64]
+                lib.lsk_mpi_alltoallv.argtypes = [i32, vp, vp, vp, vp, vp, vp, i64, i32]
+                lib.lsk_mpi_sendrecv.argtypes = [i32, vp, vp, vp, i32, vp, vp, vp, i64]
+                _mpi_lib = lib
+    return _mpi_lib
+
+
 class NativeError(RuntimeError):
     pass
 

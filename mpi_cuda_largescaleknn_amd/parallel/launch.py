@@ -6,8 +6,9 @@ Accepted launchers (all run the same code):
   (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* from the environment);
 * ``mpirun -n N bin/hipKNN_unorderedData ...`` — MPICH (PMI_RANK/PMI_SIZE) or Open MPI
   (OMPI_COMM_WORLD_*) environment, rendezvous on MASTER_ADDR (default 127.0.0.1) /
-  MASTER_PORT (default 29511); MPI itself is not used (the reference's MPI_Init /
-  MPIComm, unorderedDataVariant.cu:30-39, 107);
+  MASTER_PORT (default 29511); MPI itself carries data only with
+  ``LSKNN_DIST_BACKEND=mpi`` (the reference's MPI_Init / MPIComm,
+  unorderedDataVariant.cu:30-39, 107);
 * a plain single process.
 
 Device selection follows the reference's ``-g G`` (device = rank % G,
@@ -17,6 +18,8 @@ unorderedDataVariant.cu:138-143); without ``-g`` the local rank picks the device
 The process group is RCCL (``nccl``) for GPU runs and gloo for CPU runs.
 ``LSKNN_DIST_BACKEND=rccl`` uses the native RCCL communicator instead (parallel/rccl.py:
 RCCL called from C++ on the pipeline's own streams; a gloo group for control).
+``LSKNN_DIST_BACKEND=mpi`` moves the data with MPI (parallel/mpi.py, the native host-staged
+communicator; launch with mpirun).
 ``LSKNN_DIST_BACKEND=gloo`` forces gloo with GPU data (collectives staged through host
 memory, see TorchComm): the only way to run several GPU ranks on one device, since RCCL
 refuses two ranks on the same GPU.
@@ -120,6 +123,7 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
     fault = F.parse_fault(os.environ.get("LSKNN_FAULT"))
     store = watchdog = None
     if size > 1 or force_distributed:
+        port_given = bool(os.environ.get("MASTER_PORT"))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(size)
@@ -127,8 +131,25 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = datetime.timedelta(seconds=F.timeout_s())
         backend = os.environ.get("LSKNN_DIST_BACKEND", "nccl" if use_gpu else "gloo")
-        if backend not in ("nccl", "gloo", "rccl"):
-            raise ValueError(f"LSKNN_DIST_BACKEND must be nccl, rccl or gloo, not {backend!r}")
+        if backend not in ("nccl", "gloo", "rccl", "mpi"):
+            raise ValueError(f"LSKNN_DIST_BACKEND must be nccl, rccl, gloo or mpi, not {backend!r}")
+        if backend == "mpi":
+            # native MPI host communicator (parallel/mpi.py): the data path is MPI (the
+            # reference's transport, host-staged); rank / size come from MPI_COMM_WORLD;
+            # a gloo group on a port broadcast over MPI carries the store and the watchdog
+            # (a rank that exits early makes mpirun end the others)
+            from . import mpi as M
+            comm = M.MpiComm(device, force=force_distributed)
+            if (comm.rank, comm.size) != (rank, size):
+                raise RuntimeError(f"MPI_COMM_WORLD says rank {comm.rank} of {comm.size}, the launcher "
+                                   f"environment {rank} of {size}")
+            port = M.bcast_port(rank)
+            if not port_given:
+                os.environ["MASTER_PORT"] = str(port)
+            dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
+            store = dist.distributed_c10d._get_default_store()
+            watchdog = F.Watchdog(rank, size, store).start()
+            return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
         if backend == "rccl":
             # native RCCL communicator (parallel/rccl.py); a gloo group carries the store,
             # the watchdog and host-side control
@@ -195,6 +216,9 @@ def finalize(launch: Launch) -> None:
         if hasattr(inner, "destroy"):  # native RCCL communicator
             inner.destroy()
         dist.destroy_process_group()
+        if getattr(inner, "backend", None) == "mpi":
+            from . import mpi as M
+            M.finalize()
 
 
 def fail(launch: Launch, exc: BaseException) -> None:
