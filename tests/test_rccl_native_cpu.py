@@ -55,9 +55,9 @@ def test_rccl_comm_needs_gpu():
 def test_unknown_backend_rejected(monkeypatch):
     from mpi_cuda_largescaleknn_amd.parallel import launch as LA
     saved = dict(os.environ)  # init exports RANK / WORLD_SIZE / MASTER_* before it fails
-    monkeypatch.setenv("LSKNN_DIST_BACKEND", "mpi")
+    monkeypatch.setenv("LSKNN_DIST_BACKEND", "bogus")
     try:
-        with pytest.raises(ValueError, match="nccl, rccl or gloo"):
+        with pytest.raises(ValueError, match="nccl, rccl, gloo or mpi"):
             LA.init(device_pref="cpu", force_distributed=True)
     finally:
         for k in set(os.environ) - set(saved):
