@@ -39,7 +39,10 @@ namespace {
 using lsk::bitsf;
 using lsk::fbits;
 
-constexpr int kWavesPerBlock = 4;
+#ifndef LSK_ROWS_WPB
+#define LSK_ROWS_WPB 2
+#endif
+constexpr int kWavesPerBlock = LSK_ROWS_WPB;
 constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #ifndef LSK_ROWS_BINS
 #define LSK_ROWS_BINS 40
