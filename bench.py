@@ -14,6 +14,14 @@ clock: host points -> H2D -> (unordered variant) spatial redistribution + bucket
 k-NN + halo exchange + result return -> distances back in host memory. W untimed warmup
 steps, then K steps bracketed by barrier + device sync; the max over ranks is reported.
 
+Pipelined (default for the unordered halo pipeline on GPUs, --pipeline): the bench is a
+stream of point sets — two different synthetic sets alternate step by step, and while
+step i runs its k-NN on the compute stream, step i+1's points are copied host -> device
+on a copy stream (PCIe H2D does not compete with the VALU-bound k-NN). Every step still uploads, builds, queries and
+returns its whole set; the first set's upload is inside the timed region, and both sets'
+last outputs are verified. ms_per_step is then the per-set time of the stream; the
+instrumented step below gives the single-set latency.
+
 After the timed region (untimed): one instrumented step (per-phase times, max over
 ranks; halo sizes; per-rank k-NN ms) and a brute-force check of 256 sampled outputs
 against all points (utils/verify.py, `sampled_exact`). Rank 0 prints one JSON line.
@@ -41,6 +49,7 @@ from mpi_cuda_largescaleknn_amd.utils import trace, verify  # noqa: E402
 
 HEADLINE_METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
 GEN_CHUNK = 1 << 24  # points per seeded generation chunk (global index -> seed)
+DATASET_STRIDE = 1_000_003  # seed offset of the second point set of the pipelined bench
 # "knn_local+halo_exchange": the overlapped form (pipelines.knn_with_halo) — the local k-NN
 # and the halo publish/filter/exchange on a side stream end at one mark
 PHASES = ["bounds", "partition", "alltoallv_points", "build", "knn_local", "knn_local+halo_exchange",
@@ -83,6 +92,14 @@ def parse():
                          "never a measurement")
     ap.add_argument("--force-dist", action="store_true",
                     help="multi-rank pipeline and RCCL collectives even on one rank")
+    ap.add_argument("--pipeline", type=int, default=-1,
+                    help="1 = a stream of point sets: two different synthetic sets alternate step "
+                         "by step, and the host-to-device copy of step i+1's points runs on a copy "
+                         "stream under step i's k-NN (every step still uploads, builds, queries and "
+                         "returns its whole set; the first upload is inside the timed region); "
+                         "0 = one set, each step uploads then computes (on several ranks the upload "
+                         "is streamed under the redistribution); -1 (default) = 1 for the unordered "
+                         "halo pipeline on GPUs")
     ap.add_argument("--verify", type=int, default=256,
                     help="sampled outputs checked by brute force after the timed region (0 = off)")
     return ap.parse_args()
@@ -93,17 +110,18 @@ def block_range(n_total: int, rank: int, size: int) -> tuple[int, int]:
     return n_total * rank // size, n_total * (rank + 1) // size
 
 
-def make_points(n_total: int, rank: int, size: int, device, variant: str) -> torch.Tensor:
-    """This rank's block of the global synthetic set, in pinned host memory. Chunk c of
-    the global set (GEN_CHUNK points) always comes from seed 1234 + c, so the global set
-    does not depend on the rank count (per device type)."""
+def make_points(n_total: int, rank: int, size: int, device, variant: str, dataset: int = 0) -> torch.Tensor:
+    """This rank's block of the global synthetic set number `dataset`, in pinned host
+    memory. Chunk c of the global set (GEN_CHUNK points) always comes from seed
+    1234 + c + DATASET_STRIDE * dataset, so the global set does not depend on the rank
+    count (per device type)."""
     b, e = block_range(n_total, rank, size)
     host = torch.empty((e - b, 3), dtype=torch.float32, pin_memory=device.type == "cuda")
     if e > b:
         for c in range(b // GEN_CHUNK, (e - 1) // GEN_CHUNK + 1):
             c0 = c * GEN_CHUNK
             g = torch.Generator(device=device)
-            g.manual_seed(1234 + c)
+            g.manual_seed(1234 + c + DATASET_STRIDE * dataset)
             d = torch.rand((min(GEN_CHUNK, n_total - c0), 3), generator=g, device=device,
                            dtype=torch.float32)
             lo, hi = max(b, c0), min(e, c0 + GEN_CHUNK)
@@ -136,8 +154,12 @@ def main():
     n_total = int(args.points)
     cfg = KnnConfig(k=args.k, collect_stats=args.stats)
 
-    host_pts = make_points(n_total, rank, world, device, args.variant)
-    host_out = torch.empty(host_pts.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda")
+    # pipelined stream of point sets (see --pipeline): two different synthetic sets alternate
+    pipelined = args.pipeline != 0 and device.type == "cuda" \
+        and args.variant == "unordered" and args.mode == "halo"
+    host_sets = [make_points(n_total, rank, world, device, args.variant, d) for d in range(2 if pipelined else 1)]
+    host_outs = [torch.empty(h.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda") for h in host_sets]
+    host_pts, host_out = host_sets[0], host_outs[0]
 
     info_last = None
     direct = (PL.direct_host_out_pays(args.k) if args.direct_out < 0 else bool(args.direct_out)) \
@@ -148,10 +170,13 @@ def main():
             _step()
             _sync(device)
 
-    def _step(phases: bool = args.phases):
+    def _step(phases: bool = args.phases, pts_in=None, out_h=None):
         nonlocal info_last
+        out_h = host_out if out_h is None else out_h
         info = PL.RunInfo(PL.PhaseTimer(phases, device))
-        if args.variant == "unordered" and args.mode == "halo":
+        if pts_in is not None:
+            pts = pts_in  # pipelined: this step's points already on the device
+        elif args.variant == "unordered" and args.mode == "halo":
             # the pipeline streams the host points to the device in chunks: on several
             # ranks overlapped with the all-to-all (pipelines.redistribute_stream), on one
             # with the per-chunk bounds and curve keys (pipelines.upload_keyed)
@@ -166,16 +191,16 @@ def main():
             # one rank: the kernel writes host_out directly (k >= 48); several ranks: the
             # grouped result return copies each group's rows into it under the exchange
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
-                                   out=host_out if (direct or (comm.distributed and device.type == "cuda"))
+                                   out=out_h if (direct or (comm.distributed and device.type == "cuda"))
                                    else None)
         else:
-            out = PL.prepartitioned_knn(pts, comm, cfg, info, out=host_out if direct else None)
-        if out.data_ptr() != host_out.data_ptr():
-            host_out.copy_(out, non_blocking=True)
+            out = PL.prepartitioned_knn(pts, comm, cfg, info, out=out_h if direct else None)
+        if out.data_ptr() != out_h.data_ptr():
+            out_h.copy_(out, non_blocking=True)
         info_last = info
 
     use_graph = (args.graph == 1 or (args.graph < 0 and not (args.phases or args.stats))) \
-        and not comm.distributed and device.type == "cuda" and args.mode == "halo"
+        and not comm.distributed and device.type == "cuda" and args.mode == "halo" and not pipelined
     graph = None
     if use_graph:
         # warm up on a side stream (allocator + library state), then capture one whole
@@ -200,14 +225,41 @@ def main():
             with trace.range("lsknn:step"):
                 graph.replay()
                 _sync(device)
+    elif pipelined:
+        # step i: wait for its points (copy stream), start the upload of step i+1's set
+        # into the other device buffer (after step i-1, which read that buffer), then
+        # bounds -> tree -> k-NN -> results to host of set i on the compute stream
+        copy_stream = torch.cuda.Stream(device)
+        dbuf = [torch.empty(h.shape, dtype=h.dtype, device=device) for h in host_sets]
+
+        def prefetch(j):
+            copy_stream.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(copy_stream):
+                dbuf[j % 2].copy_(host_sets[j % 2], non_blocking=True)
+
+        def run_steps(n):
+            if n:
+                prefetch(0)  # the first set's upload is part of the run
+            for i in range(n):
+                with trace.range("lsknn:step"):
+                    torch.cuda.current_stream(device).wait_stream(copy_stream)
+                    if i + 1 < n:
+                        prefetch(i + 1)
+                    _step(pts_in=dbuf[i % 2], out_h=host_outs[i % 2])
+                    _sync(device)
+
+        run_steps(args.warmup)
     else:
         for _ in range(args.warmup):
             step()
     comm.barrier()
     _sync(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if pipelined:
+        run_steps(args.steps)
+    else:
+        for _ in range(args.steps):
+            step()
     comm.barrier()
     _sync(device)
     elapsed = time.perf_counter() - t0
@@ -221,8 +273,10 @@ def main():
     if graph is not None:
         E.verify_captured_failures(clear=True)  # raises if a replay overflowed a failure list
         heavy_unrefined = E.captured_heavy_cells(clear=True)
-    finite_t = torch.tensor([0 if host_out.numel() == 0 or bool(torch.isfinite(host_out).all()) else 1],
-                            dtype=torch.int64, device=device)
+    # the sets the timed steps wrote last (pipelined: both sets when K >= 2)
+    written = sorted({(args.steps - 1 - j) % len(host_sets) for j in range(min(args.steps, len(host_sets)))})
+    finite_t = torch.tensor([sum(0 if host_outs[d].numel() == 0 or bool(torch.isfinite(host_outs[d]).all()) else 1
+                                 for d in written)], dtype=torch.int64, device=device)
     comm.allreduce_(finite_t, "sum")
     finite = int(finite_t.item()) == 0
 
@@ -230,7 +284,11 @@ def main():
     check = None
     if args.verify > 0 and args.variant == "unordered":
         b, _ = block_range(n_total, rank, world)
-        check = verify.sampled_exact(comm, host_pts, host_out, b, n_total, args.k, args.verify)
+        for d in written:
+            c = verify.sampled_exact(comm, host_sets[d], host_outs[d], b, n_total, args.k, args.verify)
+            check = c if check is None else {"samples": check["samples"] + c["samples"],
+                                             "exact": check["exact"] + c["exact"],
+                                             "mismatch_ids": check["mismatch_ids"] + c["mismatch_ids"]}
     detail = instrumented_detail(comm, lambda: (_step(phases=True), _sync(device)), lambda: info_last)
     if rank == 0:
         if args.phases or args.stats:
@@ -248,7 +306,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "fp32",
-            "data": "synthetic uniform-random float3 in [0,1)^3 (pinned host memory), no file I/O",
+            "data": "synthetic uniform-random float3 in [0,1)^3 (pinned host memory), no file I/O"
+                    + ("; two different point sets alternate step by step" if pipelined else ""),
             "config": {
                 "model": f"{args.variant}Data k-th-NN distance, k={args.k}",
                 "global_batch": n_total,
@@ -260,6 +319,7 @@ def main():
                 "comm": (getattr(getattr(comm, "inner", comm), "backend", "single")
                          if comm.distributed else "single"),
                 "hip_graph": graph is not None,
+                "pipelined": pipelined,
                 "heavy_cells_unrefined": heavy_unrefined,
                 "all_finite": finite,
                 "sampled_exact": (f"{check['exact']}/{check['samples']}" if check else None),

@@ -50,7 +50,8 @@ def test_bench_single_gpu_graph_and_eager(graph):
     """The driver's default single-GPU bench path: the step captured as a HIP graph (or
     eager), distances finite, the graph flag reported."""
     out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "3", "--warmup", "1",
-                          "--graph", graph], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+                          "--graph", graph, "--pipeline", "0"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                         timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = _json_line(out.stdout)
     assert rec["n_gpus"] == 1 and rec["value"] > 0
@@ -60,13 +61,41 @@ def test_bench_single_gpu_graph_and_eager(graph):
 
 
 @pytest.mark.gpu
+def test_bench_single_gpu_pipelined_default():
+    """The default single-GPU bench: a stream of two alternating point sets, step i+1's
+    upload under step i's k-NN; both sets' outputs of the last two steps are checked."""
+    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "3", "--warmup", "1"],
+                         cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["config"]["pipelined"] is True and rec["config"]["hip_graph"] is False
+    assert rec["config"]["all_finite"] is True
+    assert rec["config"]["sampled_exact"] == "512/512"
+    assert "two different point sets" in rec["data"]
+
+
+@pytest.mark.gpu
+def test_bench_pipelined_forced_rccl_single_gpu():
+    """--pipeline 1 on the multi-rank path (1-rank RCCL group): device-resident input per
+    step, plain (non-streamed) redistribution, both sets exact."""
+    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
+                          "--force-dist", "--pipeline", "1"],
+                         cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port())),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["config"]["pipelined"] is True
+    assert rec["config"]["sampled_exact"] == "512/512"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("backend", ["nccl", "rccl"])
 def test_bench_forced_rccl_single_gpu(backend):
     """One rank through the multi-rank pipeline on a real 1-rank RCCL group: every
     collective of the step (all-reduce, all-gather, all-to-all-v) runs on RCCL — through
     torch.distributed ("nccl") or the native communicator ("rccl", parallel/rccl.py)."""
     out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
-                          "--force-dist"], cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1",
+                          "--force-dist", "--pipeline", "0"], cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1",
                                                                MASTER_PORT=str(_free_port()),
                                                                LSKNN_DIST_BACKEND=backend),
                          capture_output=True, text=True, timeout=300)
@@ -124,3 +153,21 @@ def test_bench_four_ranks_streamed_uneven_chunks():
     assert rec["n_gpus"] == 4 and rec["config"]["global_batch"] == 30001
     assert rec["config"]["sampled_exact"] == "256/256"
     assert sum(rec["detail"]["owned_points_per_rank"]) == 30001
+
+
+@pytest.mark.gpu
+def test_bench_two_gpu_ranks_pipelined_gloo():
+    """The driver's multi-rank launch (torchrun, 2 ranks) with the default pipelined
+    stream, both ranks on the one GPU of the box over a host-staged gloo group (RCCL
+    refuses two ranks on one device): both sets' sampled outputs exact."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--points", "400000", "--steps", "3", "--warmup", "1"]
+    out = subprocess.run(cmd, cwd=ROOT, env=dict(_env(), LSKNN_DIST_BACKEND="gloo"), capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["pipelined"] is True
+    assert rec["config"]["all_finite"] is True
+    assert rec["config"]["sampled_exact"] == "512/512"
+    assert sum(rec["detail"]["owned_points_per_rank"]) == 400000
