@@ -17,7 +17,7 @@ steps, then K steps bracketed by barrier + device sync; the max over ranks is re
 Pipelined (default for the unordered halo pipeline on GPUs, --pipeline): the bench is a
 stream of point sets — two different synthetic sets alternate step by step, and while
 step i runs its k-NN on the compute stream, step i+1's points are copied host -> device
-on a copy stream (PCIe H2D does not compete with the VALU-bound k-NN). Every step still uploads, builds, queries and
+(PCIe H2D does not compete with the VALU-bound k-NN). Every step still uploads, builds, queries and
 returns its whole set; the first set's upload is inside the timed region, and both sets'
 last outputs are verified. ms_per_step is then the per-set time of the stream; the
 instrumented step below gives the single-set latency.
@@ -225,10 +225,42 @@ def main():
             with trace.range("lsknn:step"):
                 graph.replay()
                 _sync(device)
+    elif pipelined and not comm.distributed and os.environ.get("LSKNN_PIPE_BUILD", "0") == "1":
+        # (A/B option, off by default) one rank: step i+1's upload AND index build (bounds,
+        # keys, sort, tree) on a high-priority side stream under step i's k-NN; the k-NN
+        # launch is queued first and its failure-word check deferred, so the build's own
+        # host sync (over-full cell check) waits for the side stream only. Measured slower
+        # on 1B (698.0 / 698.0 vs 706.2 / 707.4 Mpts/s copy-only, profiles/r2_s3_pipe): the
+        # sort / gather blocks take CU slots and LDS from the VALU-bound k-NN grid
+        side = torch.cuda.Stream(device, priority=-1)
+        dbuf = torch.empty(host_sets[0].shape, dtype=host_sets[0].dtype, device=device)
+
+        def build_next(j):
+            with torch.cuda.stream(side):
+                dbuf.copy_(host_sets[j % 2], non_blocking=True)
+                return PL.local_build(dbuf, comm, cfg, n_total)
+
+        def run_steps(n):
+            nxt = build_next(0) if n else None  # the first set's upload + build are timed
+            for i in range(n):
+                with trace.range("lsknn:step"):
+                    torch.cuda.current_stream(device).wait_stream(side)
+                    index, hint2 = nxt
+                    deferred = []
+                    res = PL.local_query(index, hint2, cfg, out=host_outs[i % 2] if direct else None,
+                                         deferred=deferred)
+                    if res.data_ptr() != host_outs[i % 2].data_ptr():
+                        host_outs[i % 2].copy_(res, non_blocking=True)
+                    nxt = build_next(i + 1) if i + 1 < n else None
+                    E.settle(deferred)
+                    _sync(device)
+                    del index, hint2, res
+
+        run_steps(args.warmup)
     elif pipelined:
-        # step i: wait for its points (copy stream), start the upload of step i+1's set
-        # into the other device buffer (after step i-1, which read that buffer), then
-        # bounds -> tree -> k-NN -> results to host of set i on the compute stream
+        # several ranks: step i waits for its points (copy stream), starts the upload of
+        # step i+1's set into the other device buffer (after step i-1, which read that
+        # buffer), then redistribution -> tree -> k-NN + halo -> return of set i
         copy_stream = torch.cuda.Stream(device)
         dbuf = [torch.empty(h.shape, dtype=h.dtype, device=device) for h in host_sets]
 

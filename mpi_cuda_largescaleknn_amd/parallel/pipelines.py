@@ -652,6 +652,42 @@ def upload_keyed(host_pts: torch.Tensor, dev: torch.device, chunk: int | None = 
     return pts, (keys, iota), box
 
 
+def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
+                info: RunInfo | None = None) -> tuple[E.LocalIndex, float | torch.Tensor]:
+    """Single-rank first half: points (host or device) -> device, bounds, radius hint,
+    Hilbert-sorted bucket tree. Everything is enqueued on the current stream; the one host
+    sync is the over-full-cell check after the sort (see knn_engine.refine_heavy_cells),
+    which waits for this stream only — so a caller can build the next point set on a side
+    stream while the current set's k-NN runs (bench.py --pipeline)."""
+    info = info or RunInfo(PhaseTimer(False, comm.device))
+    dev = comm.device
+    n_local = points.shape[0]
+    if points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
+        dpts, keys, box = upload_keyed(points, dev)
+        points = dpts
+    else:
+        points = points.to(dev, non_blocking=True) if points.device != dev else points
+        box, keys = global_box(points, comm), None
+    hint2 = E.radius_hint(box, n_total, cfg.k)
+    info.timer.mark("bounds")
+    info.counts["owned_points"] = n_local
+    index = E.build_index(points, box, keys=keys)
+    info.timer.mark("build")
+    return index, hint2
+
+
+def local_query(index: E.LocalIndex, hint2, cfg: E.KnnConfig, info: RunInfo | None = None,
+                out: torch.Tensor | None = None, deferred: list | None = None) -> torch.Tensor:
+    """Single-rank second half: the k-NN kernel writes the final distances in input order
+    (fused scatter) into `out` (see unordered_knn). `deferred`: as in knn_engine.query."""
+    info = info or RunInfo(PhaseTimer(False, index.device))
+    out = _check_out(out, index.n, index.pts)
+    E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out,
+            deferred=deferred)
+    info.timer.mark("knn_local")
+    return out
+
+
 def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
                   n_total: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """k-th-NN distance of every local point (input order) for a globally unordered set
@@ -674,22 +710,8 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     streamed = comm.distributed and (points.device != comm.device or FORCE_STREAM)
     dev = comm.device
     if not comm.distributed:
-        if points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
-            dpts, keys, box = upload_keyed(points, dev)
-            points = dpts
-        else:
-            points = points.to(dev, non_blocking=True) if points.device != dev else points
-            box, keys = global_box(points, comm), None
-        hint2 = E.radius_hint(box, n_total, cfg.k)
-        info.timer.mark("bounds")
-        info.counts["owned_points"] = n_local
-        index = E.build_index(points, box, keys=keys)
-        info.timer.mark("build")
-        # one rank: the k-NN kernel writes the final distances in input order (fused scatter)
-        out = _check_out(out, n_local, points)
-        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
-        info.timer.mark("knn_local")
-        return out
+        index, hint2 = local_build(points, comm, cfg, n_total, info)
+        return local_query(index, hint2, cfg, info, out)
     if not streamed and points.device != dev:
         points = points.to(dev, non_blocking=True)
     if streamed:
