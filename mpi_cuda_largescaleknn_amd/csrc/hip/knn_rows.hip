@@ -31,7 +31,7 @@
 //  Inner-loop cost per candidate and lane: 6 VALU for d² (DPP broadcast folded into the
 //  subtracts) + 5 VALU + 1 exec-masked ds_add for the histogram when in range (compiled
 //  with -fno-slp-vectorize: packed-math ops cannot take DPP operands). 7 waves/SIMD
-//  (72 VGPRs, 22 KB LDS/block).
+//  (72 VGPRs, 5.6 KB LDS per wave, 2-wave blocks).
 #include "dev.h"
 
 namespace {
@@ -39,6 +39,9 @@ namespace {
 using lsk::bitsf;
 using lsk::fbits;
 
+// waves per workgroup: a block holds its LDS until its last wave ends, so 2-wave blocks
+// free slots sooner when waves differ in length (1B bench 633.5/633.9 vs 629.7/631.5
+// Mpts/s with 4; 1 wave per block is slower: profiles/r2_s3_wpb)
 #ifndef LSK_ROWS_WPB
 #define LSK_ROWS_WPB 2
 #endif
@@ -48,7 +51,7 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #define LSK_ROWS_BINS 40
 #endif
 #ifndef LSK_ROWS_MINW
-// 7 waves/SIMD: 40 bins keep the LDS at 22 KB/block (7 blocks/CU) and the allocator fits
+// 7 waves/SIMD: 40 bins keep the LDS at 5.6 KB per wave (28 waves/CU) and the allocator fits
 // 72 VGPRs with 4-candidate batches (its spills sit in per-pass code, not in the inner
 // loops). 1e8 pts, k=100 (round 1): 5 waves 0.166 s, 6 waves 0.149-0.152 s, 7 waves
 // 0.147 s, 8 waves (36 bins) 0.155 s; round 2: 8 waves 0.137 vs 7 waves 0.126 s. The
@@ -1422,7 +1425,7 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
   const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
-  // Row work-queue capacity 32 entries per row: 22 KB of LDS per 4-wave block, 7 blocks
+  // Row work-queue capacity 32 entries per row: 5.6 KB of LDS per wave, 28 waves
   // per CU. One instance per tree count: the single-tree one (every local pass) has no
   // per-lane tree selects in its step loop; the two-tree one serves halo re-queries.
   if (A.ntrees > 1)
