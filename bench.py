@@ -170,7 +170,9 @@ def main():
             _step()
             _sync(device)
 
-    def _step(phases: bool = args.phases, pts_in=None, out_h=None):
+    def _step(phases: bool = args.phases, pts_in=None, out_h=None, defer_out: bool = False):
+        """One step; defer_out (several ranks): return the device result instead of
+        copying it to out_h (the pipelined loop copies it on its own stream)."""
         nonlocal info_last
         out_h = host_out if out_h is None else out_h
         info = PL.RunInfo(PL.PhaseTimer(phases, device))
@@ -190,14 +192,17 @@ def main():
         elif args.variant == "unordered":
             # one rank: the kernel writes host_out directly (k >= 48); several ranks: the
             # grouped result return copies each group's rows into it under the exchange
+            want_host = direct or (comm.distributed and device.type == "cuda")
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
-                                   out=out_h if (direct or (comm.distributed and device.type == "cuda"))
-                                   else None)
+                                   out=out_h if want_host and not defer_out else None)
         else:
             out = PL.prepartitioned_knn(pts, comm, cfg, info, out=out_h if direct else None)
+        info_last = info
+        if defer_out:
+            return out
         if out.data_ptr() != out_h.data_ptr():
             out_h.copy_(out, non_blocking=True)
-        info_last = info
+        return out_h
 
     use_graph = (args.graph == 1 or (args.graph < 0 and not (args.phases or args.stats))) \
         and not comm.distributed and device.type == "cuda" and args.mode == "halo" and not pipelined
@@ -258,10 +263,13 @@ def main():
 
         run_steps(args.warmup)
     elif pipelined:
-        # several ranks: step i waits for its points (copy stream), starts the upload of
-        # step i+1's set into the other device buffer (after step i-1, which read that
-        # buffer), then redistribution -> tree -> k-NN + halo -> return of set i
+        # step i waits for its points (copy stream), starts the upload of step i+1's set
+        # into the other device buffer (after step i-1, which read that buffer), then
+        # (redistribution ->) tree -> k-NN (+ halo -> return) of set i. One rank: the
+        # kernel writes the distances to pinned host memory itself. Several ranks: the
+        # returned distances go to host memory on a third stream, under step i+1.
         copy_stream = torch.cuda.Stream(device)
+        out_stream = torch.cuda.Stream(device)
         dbuf = [torch.empty(h.shape, dtype=h.dtype, device=device) for h in host_sets]
 
         def prefetch(j):
@@ -277,8 +285,18 @@ def main():
                     torch.cuda.current_stream(device).wait_stream(copy_stream)
                     if i + 1 < n:
                         prefetch(i + 1)
-                    _step(pts_in=dbuf[i % 2], out_h=host_outs[i % 2])
-                    _sync(device)
+                    if comm.distributed:
+                        res = _step(pts_in=dbuf[i % 2], defer_out=True)
+                        out_stream.wait_stream(torch.cuda.current_stream(device))
+                        with torch.cuda.stream(out_stream):
+                            host_outs[i % 2].copy_(res, non_blocking=True)
+                        res.record_stream(out_stream)  # kept until the copy is done
+                        del res
+                        torch.cuda.current_stream(device).synchronize()
+                    else:
+                        _step(pts_in=dbuf[i % 2], out_h=host_outs[i % 2])
+                        _sync(device)
+            _sync(device)  # the last results are in host memory
 
         run_steps(args.warmup)
     else:
