@@ -22,9 +22,10 @@ returns its whole set; the first set's upload is inside the timed region, and bo
 last outputs are verified. ms_per_step is then the per-set time of the stream; the
 instrumented step below gives the single-set latency.
 
-After the timed region (untimed): one instrumented step (per-phase times, max over
-ranks; halo sizes; per-rank k-NN ms) and a brute-force check of 256 sampled outputs
-against all points (utils/verify.py, `sampled_exact`). Rank 0 prints one JSON line.
+After the timed region (untimed): one instrumented step of the timed path (per-phase
+times, max over ranks; halo sizes; per-rank k-NN ms; pipelined: from device-resident
+points) and a brute-force check of 256 sampled outputs per verified set against all
+points (utils/verify.py, `sampled_exact`). Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -339,7 +340,13 @@ def main():
             check = c if check is None else {"samples": check["samples"] + c["samples"],
                                              "exact": check["exact"] + c["exact"],
                                              "mismatch_ids": check["mismatch_ids"] + c["mismatch_ids"]}
-    detail = instrumented_detail(comm, lambda: (_step(phases=True), _sync(device)), lambda: info_last)
+    # the instrumented step takes the timed path: pipelined steps start from points already
+    # on the device (their upload ran under the previous step), so this one does too
+    pts_dev = host_pts.to(device) if pipelined else None
+    _sync(device)
+    detail = instrumented_detail(comm, lambda: (_step(phases=True, pts_in=pts_dev), _sync(device)),
+                                 lambda: info_last)
+    del pts_dev
     if rank == 0:
         if args.phases or args.stats:
             print(json.dumps({"phases_s": info_last.timer.times, "counts": info_last.counts,
