@@ -46,6 +46,7 @@ from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import launch as LA  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel.stream import SetStream  # noqa: E402
 from mpi_cuda_largescaleknn_amd.utils import trace, verify  # noqa: E402
 
 HEADLINE_METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
@@ -171,9 +172,7 @@ def main():
             _step()
             _sync(device)
 
-    def _step(phases: bool = args.phases, pts_in=None, out_h=None, defer_out: bool = False):
-        """One step; defer_out (several ranks): return the device result instead of
-        copying it to out_h (the pipelined loop copies it on its own stream)."""
+    def _step(phases: bool = args.phases, pts_in=None, out_h=None):
         nonlocal info_last
         out_h = host_out if out_h is None else out_h
         info = PL.RunInfo(PL.PhaseTimer(phases, device))
@@ -193,17 +192,14 @@ def main():
         elif args.variant == "unordered":
             # one rank: the kernel writes host_out directly (k >= 48); several ranks: the
             # grouped result return copies each group's rows into it under the exchange
-            want_host = direct or (comm.distributed and device.type == "cuda")
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
-                                   out=out_h if want_host and not defer_out else None)
+                                   out=out_h if (direct or (comm.distributed and device.type == "cuda"))
+                                   else None)
         else:
             out = PL.prepartitioned_knn(pts, comm, cfg, info, out=out_h if direct else None)
-        info_last = info
-        if defer_out:
-            return out
         if out.data_ptr() != out_h.data_ptr():
             out_h.copy_(out, non_blocking=True)
-        return out_h
+        info_last = info
 
     use_graph = (args.graph == 1 or (args.graph < 0 and not (args.phases or args.stats))) \
         and not comm.distributed and device.type == "cuda" and args.mode == "halo" and not pipelined
@@ -231,73 +227,15 @@ def main():
             with trace.range("lsknn:step"):
                 graph.replay()
                 _sync(device)
-    elif pipelined and not comm.distributed and os.environ.get("LSKNN_PIPE_BUILD", "0") == "1":
-        # (A/B option, off by default) one rank: step i+1's upload AND index build (bounds,
-        # keys, sort, tree) on a high-priority side stream under step i's k-NN; the k-NN
-        # launch is queued first and its failure-word check deferred, so the build's own
-        # host sync (over-full cell check) waits for the side stream only. Measured slower
-        # on 1B (698.0 / 698.0 vs 706.2 / 707.4 Mpts/s copy-only, profiles/r2_s3_pipe): the
-        # sort / gather blocks take CU slots and LDS from the VALU-bound k-NN grid
-        side = torch.cuda.Stream(device, priority=-1)
-        dbuf = torch.empty(host_sets[0].shape, dtype=host_sets[0].dtype, device=device)
-
-        def build_next(j):
-            with torch.cuda.stream(side):
-                dbuf.copy_(host_sets[j % 2], non_blocking=True)
-                return PL.local_build(dbuf, comm, cfg, n_total)
-
-        def run_steps(n):
-            nxt = build_next(0) if n else None  # the first set's upload + build are timed
-            for i in range(n):
-                with trace.range("lsknn:step"):
-                    torch.cuda.current_stream(device).wait_stream(side)
-                    index, hint2 = nxt
-                    deferred = []
-                    res = PL.local_query(index, hint2, cfg, out=host_outs[i % 2] if direct else None,
-                                         deferred=deferred)
-                    if res.data_ptr() != host_outs[i % 2].data_ptr():
-                        host_outs[i % 2].copy_(res, non_blocking=True)
-                    nxt = build_next(i + 1) if i + 1 < n else None
-                    E.settle(deferred)
-                    _sync(device)
-                    del index, hint2, res
-
-        run_steps(args.warmup)
     elif pipelined:
-        # step i waits for its points (copy stream), starts the upload of step i+1's set
-        # into the other device buffer (after step i-1, which read that buffer), then
-        # (redistribution ->) tree -> k-NN (+ halo -> return) of set i. One rank: the
-        # kernel writes the distances to pinned host memory itself. Several ranks: the
-        # returned distances go to host memory on a third stream, under step i+1.
-        copy_stream = torch.cuda.Stream(device)
-        out_stream = torch.cuda.Stream(device)
-        dbuf = [torch.empty(h.shape, dtype=h.dtype, device=device) for h in host_sets]
-
-        def prefetch(j):
-            copy_stream.wait_stream(torch.cuda.current_stream(device))
-            with torch.cuda.stream(copy_stream):
-                dbuf[j % 2].copy_(host_sets[j % 2], non_blocking=True)
+        # stream of sets (parallel/stream.py): set i+1's upload under set i's build and
+        # k-NN; several ranks: set i's results to host under set i+1
+        runner = SetStream(comm, cfg, direct_out=direct)
 
         def run_steps(n):
-            if n:
-                prefetch(0)  # the first set's upload is part of the run
-            for i in range(n):
-                with trace.range("lsknn:step"):
-                    torch.cuda.current_stream(device).wait_stream(copy_stream)
-                    if i + 1 < n:
-                        prefetch(i + 1)
-                    if comm.distributed:
-                        res = _step(pts_in=dbuf[i % 2], defer_out=True)
-                        out_stream.wait_stream(torch.cuda.current_stream(device))
-                        with torch.cuda.stream(out_stream):
-                            host_outs[i % 2].copy_(res, non_blocking=True)
-                        res.record_stream(out_stream)  # kept until the copy is done
-                        del res
-                        torch.cuda.current_stream(device).synchronize()
-                    else:
-                        _step(pts_in=dbuf[i % 2], out_h=host_outs[i % 2])
-                        _sync(device)
-            _sync(device)  # the last results are in host memory
+            with trace.range("lsknn:steps"):
+                runner.run([host_sets[i % 2] for i in range(n)], [host_outs[i % 2] for i in range(n)],
+                           n_totals=[n_total] * n)
 
         run_steps(args.warmup)
     else:
