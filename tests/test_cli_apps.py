@@ -160,3 +160,36 @@ def test_gpu_app_forced_rccl_matches_cpu(data, backend):
                        text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     assert out.read_bytes() == (data / "ref.float").read_bytes()
+
+
+STREAM = "mpi_cuda_largescaleknn_amd.apps.stream"
+
+
+@pytest.mark.parametrize("nproc", [1, 3])
+def test_stream_app_matches_unordered_per_file(data, tmp_path, nproc):
+    """hipKNN_stream over three files (one repeated): each output file has the same bytes as
+    hipKNN_unorderedData run on that file alone."""
+    run([TOOLS, "gen", str(tmp_path / "b.float3"), "-n", "5000", "--seed", "9"])
+    run([UN, str(tmp_path / "b.float3"), "-o", str(tmp_path / "b_ref.float"), "-k", "20", "--device", "cpu"])
+    files = [str(data / "pts.float3"), str(tmp_path / "b.float3"), str(data / "pts.float3")]
+    p = run([STREAM, *files, "-o", str(tmp_path / "s"), "-k", "20", "--device", "cpu"], nproc=nproc)
+    assert p.stdout.count("done all queries...") == nproc
+    refs = [data / "ref.float", tmp_path / "b_ref.float", data / "ref.float"]
+    for i, ref in enumerate(refs):
+        assert (tmp_path / f"s_{i:06d}.float").read_bytes() == ref.read_bytes(), i
+
+
+def test_stream_app_errors(data, tmp_path):
+    p = run([STREAM, str(data / "pts.float3"), "-o", str(tmp_path / "x"), "-k", "0"], check=False)
+    assert p.returncode != 0
+    p = run([STREAM, str(tmp_path / "missing.float3"), "-o", str(tmp_path / "x"), "-k", "4", "--device", "cpu"],
+            check=False)
+    assert p.returncode == 1
+
+
+@pytest.mark.gpu
+def test_stream_app_gpu_matches_cpu(data, tmp_path):
+    files = [str(data / "pts.float3"), str(data / "pts.float3")]
+    run([STREAM, *files, "-o", str(tmp_path / "g"), "-k", "20", "--device", "cuda"])
+    for i in range(2):
+        assert (tmp_path / f"g_{i:06d}.float").read_bytes() == (data / "ref.float").read_bytes()
