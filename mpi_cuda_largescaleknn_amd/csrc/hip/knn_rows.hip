@@ -961,7 +961,10 @@ __device__ __forceinline__ float bcast64(float v, uint32_t j) {
 
 __device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k,
                                                      bool &dup) {
-  constexpr int M = 8;
+#ifndef LSK_EST_M
+#define LSK_EST_M 8
+#endif
+  constexpr int M = LSK_EST_M;  // nearest group members kept for the estimate
   float best[M];
 #pragma unroll
   for (int i = 0; i < M; i++) best[i] = __builtin_inff();
