@@ -1409,6 +1409,10 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 
 }  // namespace
 
+#ifndef LSK_RCAP
+#define LSK_RCAP 32  // row queue capacity (entries per row, a power of two <= 32)
+#endif
+
 extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const lsk_knn_args &A = *args;
   if (A.k < 1 || A.k > 65535) {
@@ -1432,9 +1436,9 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   // per CU. One instance per tree count: the single-tree one (every local pass) has no
   // per-lane tree selects in its step loop; the two-tree one serves halo re-queries.
   if (A.ntrees > 1)
-    knn_rows_kernel<32, 2><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+    knn_rows_kernel<LSK_RCAP, 2><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   else
-    knn_rows_kernel<32, 1><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+    knn_rows_kernel<LSK_RCAP, 1><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
   LSK_CHECK_LAUNCH("knn_rows");
   return 0;
 }
