@@ -518,9 +518,13 @@ def _radius_bounds(index: E.LocalIndex, cfg: E.KnnConfig) -> torch.Tensor:
 
 
 def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: float | torch.Tensor,
-                  info: RunInfo, final_out: torch.Tensor) -> torch.Tensor:
+                  info: RunInfo, final_out: torch.Tensor, hook=None) -> torch.Tensor:
     """Local k-NN of every owned query + halo exchange + re-query (distributed runs).
-    Returns the sorted d2; `final_out` receives the final distances (index.perm order)."""
+    Returns the sorted d2; `final_out` receives the final distances (index.perm order).
+    `hook(after_stream)` (overlapped GPU path): called once the local k-NN and the halo
+    exchange are queued, before the host waits for the k-NN — independent work issued
+    there (SetStream: the next point set's redistribution) runs under the k-NN; it must
+    order its collectives after `after_stream` (the halo exchange)."""
     stats = info.stats if cfg.collect_stats else None
     gpu = K.is_gpu(index.pts)
     if not OVERLAP_HALO or (gpu and torch.cuda.is_current_stream_capturing()):
@@ -548,6 +552,8 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
     recv.record_stream(cur)
     d2.record_stream(cur)
     final_out.record_stream(comp)
+    if hook is not None:
+        hook(side)
     E.settle(pend)
     info.counts["halo_overlap"] = 1
     info.timer.mark("knn_local+halo_exchange")
@@ -712,17 +718,11 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     if not comm.distributed:
         index, hint2 = local_build(points, comm, cfg, n_total, info)
         return local_query(index, hint2, cfg, info, out)
-    if not streamed and points.device != dev:
-        points = points.to(dev, non_blocking=True)
-    if streamed:
-        R = redistribute_stream(points, comm, info)
-        box, owned = R.box, R.owned
-        hint2 = E.radius_hint(box, n_total, cfg.k)
-    else:
-        box = global_box(points, comm)
-        hint2 = E.radius_hint(box, n_total, cfg.k)
-        info.timer.mark("bounds")
-        owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
+    if not streamed:
+        return compute_set(redistribute_set(points, comm, cfg, n_total, info), comm, cfg, info, out=out)
+    R = redistribute_stream(points, comm, info)
+    box, owned = R.box, R.owned
+    hint2 = E.radius_hint(box, n_total, cfg.k)
     index = E.build_index(owned, box)
     info.timer.mark("build")
     # final distances in received-row order straight from the kernels (fused scatter);
@@ -735,13 +735,66 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
         _return_grouped(R, dist_owned, comm, res, out)
         info.timer.mark("return")
         return out
-    if streamed:
-        # counts of the return are known from the send side: no count exchange
-        back, _ = comm.alltoallv(dist_owned[R.ret_index], R.ret_counts, recv_counts=R.back_counts)
-        K.scatter1(back, R.origin_index.to(torch.int32), res, finalize=False)
-    else:
-        back, _ = comm.alltoallv(dist_owned, recv_counts, recv_counts=send_counts)
-        K.scatter1(back, send_perm, res, finalize=False)
+    # counts of the return are known from the send side: no count exchange
+    back, _ = comm.alltoallv(dist_owned[R.ret_index], R.ret_counts, recv_counts=R.back_counts)
+    K.scatter1(back, R.origin_index.to(torch.int32), res, finalize=False)
+    info.timer.mark("return")
+    if out is not None:
+        out.copy_(res, non_blocking=True)
+        return out
+    return res
+
+
+@dataclass
+class Redistributed:
+    """A point set after its spatial redistribution (non-streamed multi-rank path)."""
+    n_local: int                 # this rank's input points
+    box: torch.Tensor            # global box
+    hint2: object                # radius hint (device tensor or float)
+    owned: torch.Tensor          # [m, 3] points this rank owns (received-row order)
+    recv_counts: list
+    send_perm: torch.Tensor      # local input row of each sent row
+    send_counts: list
+
+
+def redistribute_set(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
+                     info: RunInfo | None = None) -> Redistributed:
+    """First half of the multi-rank unordered pipeline on device-resident points: global
+    bounds, splitters, all-to-all-v of every point to its spatial owner. Everything is
+    queued on the current stream (collectives included)."""
+    info = info or RunInfo(PhaseTimer(False, comm.device))
+    points = points.contiguous()
+    if points.device != comm.device:
+        points = points.to(comm.device, non_blocking=True)
+    box = global_box(points, comm)
+    hint2 = E.radius_hint(box, n_total, cfg.k)
+    info.timer.mark("bounds")
+    owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
+    return Redistributed(int(points.shape[0]), box, hint2, owned, recv_counts, send_perm, send_counts)
+
+
+def compute_set(P: Redistributed, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
+                out: torch.Tensor | None = None, hook=None) -> torch.Tensor:
+    """Second half: bucket tree of the owned points, local k-NN + halo exchange + re-query,
+    distances back to their origin ranks in input order (into `out` if given). `hook`:
+    see knn_with_halo; it returns the stream its collectives ran on, and the result
+    return is ordered after it (one communicator: no concurrent collectives)."""
+    info = info or RunInfo(PhaseTimer(False, comm.device))
+    dev = comm.device
+    index = E.build_index(P.owned, P.box)
+    info.timer.mark("build")
+    dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
+    used: list = []
+    knn_with_halo(index, comm, cfg, P.hint2, info, dist_owned,
+                  hook=(lambda after: used.append(hook(after))) if hook is not None else None)
+    if hook is not None and not used:  # (a path without the overlap point: run it here)
+        used.append(hook(torch.cuda.current_stream(dev)) if K.is_gpu(dist_owned) else hook(None))
+    for st in used:
+        if st is not None:
+            torch.cuda.current_stream(dev).wait_stream(st)
+    res = torch.empty(P.n_local, dtype=torch.float32, device=dev)
+    back, _ = comm.alltoallv(dist_owned, P.recv_counts, recv_counts=P.send_counts)
+    K.scatter1(back, P.send_perm, res, finalize=False)
     info.timer.mark("return")
     if out is not None:
         out.copy_(res, non_blocking=True)

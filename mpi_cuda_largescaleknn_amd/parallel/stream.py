@@ -10,8 +10,12 @@ before ~1.4 s of index build and k-NN. `SetStream` overlaps them across sets:
   one waits for the set that last read it;
 * one rank: the k-NN kernel writes set i's distances straight into its pinned host
   output while it runs (pipelines.local_query), nothing to copy afterwards;
-* several ranks: set i's returned distances go device -> host on a third stream under
-  set i+1 (the result tensor is kept alive for that copy with record_stream).
+* several ranks: set i+1's spatial redistribution (bounds, splitters, all-to-all-v of
+  the points) is issued on a fourth stream right after set i's local k-NN and halo
+  exchange are queued, so it runs under set i's k-NN (pipelines.compute_set hook; its
+  collectives are ordered after the halo exchange and before set i's result return,
+  one communicator never has two collectives in flight); set i's returned distances go
+  device -> host on a third stream under set i+1 (kept alive with record_stream).
 
 Every set is still uploaded, redistributed (several ranks), built, queried and returned in
 full; only the order in which independent work is issued changes. On a CPU device the sets
@@ -49,6 +53,7 @@ class SetStream:
         if self.gpu:
             self.copy_stream = torch.cuda.Stream(self.device)
             self.out_stream = torch.cuda.Stream(self.device)
+            self.redist_stream = torch.cuda.Stream(self.device)
         self._dbuf: list[torch.Tensor | None] = [None, None]
         self.last_info: PL.RunInfo | None = None
 
@@ -85,6 +90,8 @@ class SetStream:
                 outputs[i].copy_(out)
                 self.last_info = info
             return
+        if self.comm.distributed:
+            return self._run_distributed(inputs, outputs, n_totals, new_info)
         cur = torch.cuda.current_stream(self.device)
         if n:
             self._prefetch(0, inputs[0])
@@ -94,20 +101,56 @@ class SetStream:
             if i + 1 < n:
                 self._prefetch(i + 1, inputs[i + 1])
             info = new_info()
-            if self.comm.distributed:
-                res = PL.unordered_knn(pts, self.comm, self.cfg, info, n_total=n_totals[i])
-                self.out_stream.wait_stream(cur)
-                with torch.cuda.stream(self.out_stream):
-                    outputs[i].copy_(res, non_blocking=True)
-                res.record_stream(self.out_stream)  # kept until its copy is done
-                del res
-                cur.synchronize()
-            else:
-                res = PL.unordered_knn(pts, self.comm, self.cfg, info, n_total=n_totals[i],
-                                       out=outputs[i] if self.direct_out else None)
-                if res.data_ptr() != outputs[i].data_ptr():
-                    outputs[i].copy_(res, non_blocking=True)
-                del res
-                torch.cuda.synchronize(self.device)
+            res = PL.unordered_knn(pts, self.comm, self.cfg, info, n_total=n_totals[i],
+                                   out=outputs[i] if self.direct_out else None)
+            if res.data_ptr() != outputs[i].data_ptr():
+                outputs[i].copy_(res, non_blocking=True)
+            del res
+            torch.cuda.synchronize(self.device)
             self.last_info = info
         torch.cuda.synchronize(self.device)  # the last results are in host memory
+
+    def _run_distributed(self, inputs, outputs, n_totals, new_info) -> None:
+        comm, cfg, dev = self.comm, self.cfg, self.device
+        cur = torch.cuda.current_stream(dev)
+        redist = self.redist_stream
+        n = len(inputs)
+        for j in range(n):  # global point counts (one small all-reduce per unknown set)
+            if n_totals[j] is None:
+                t = torch.tensor([int(inputs[j].shape[0])], dtype=torch.int64, device=dev)
+                comm.allreduce_(t, "sum")
+                n_totals[j] = int(t.item())
+        if n == 0:
+            return
+        self._prefetch(0, inputs[0])
+        cur.wait_stream(self.copy_stream)
+        P = PL.redistribute_set(self._dbuf[0], comm, cfg, n_totals[0], new_info())
+        if n > 1:
+            self._prefetch(1, inputs[1])
+        for i in range(n):
+            info = new_info()
+            nxt: dict = {}
+
+            def hook(after, j=i + 1):
+                # set j's redistribution under set i's k-NN: after the halo exchange's
+                # collectives, once set j's points are on the device
+                redist.wait_stream(after)
+                redist.wait_stream(self.copy_stream)
+                with torch.cuda.stream(redist):
+                    nxt["P"] = PL.redistribute_set(self._dbuf[j % 2], comm, cfg, n_totals[j])
+                return redist
+
+            res = PL.compute_set(P, comm, cfg, info, hook=hook if i + 1 < n else None)
+            self.out_stream.wait_stream(cur)
+            with torch.cuda.stream(self.out_stream):
+                outputs[i].copy_(res, non_blocking=True)
+            res.record_stream(self.out_stream)  # kept until its copy is done
+            del res
+            cur.synchronize()
+            redist.synchronize()
+            if i + 2 < n:  # the buffer set i was redistributed from is free again
+                self._prefetch(i + 2, inputs[i + 2])
+            cur.wait_stream(redist)
+            P = nxt.get("P")
+            self.last_info = info
+        torch.cuda.synchronize(dev)  # the last results are in host memory
