@@ -67,3 +67,34 @@ def test_stream_single_gpu(direct):
     for i, p in enumerate(S):
         assert torch.equal(outs[i], oracle(p, k)), i
     assert runner.last_info is not None
+
+
+@pytest.mark.parametrize("size", [1, 3])
+def test_compute_set_hook_redistributes_next_set_cpu(size):
+    """The multi-rank two-phase API with the overlap hook (SetStream's GPU path): set B is
+    redistributed from inside set A's compute phase; both results equal the oracle."""
+    k = 8
+    cfg = E.KnnConfig(k=k, publish_levels=4)
+    A = GENERATORS["uniform"](4000, seed=5)
+    B = GENERATORS["clustered"](5000, seed=6)
+
+    def part(p, comm):
+        b, e = p.shape[0] * comm.rank // comm.size, p.shape[0] * (comm.rank + 1) // comm.size
+        return p[b:e].contiguous()
+
+    def fn(comm):
+        comm.force = True  # the multi-rank path even on one rank
+        PA = PL.redistribute_set(part(A, comm), comm, cfg, A.shape[0])
+        nxt = {}
+
+        def hook(after):
+            nxt["P"] = PL.redistribute_set(part(B, comm), comm, cfg, B.shape[0])
+            return None
+
+        ra = PL.compute_set(PA, comm, cfg, hook=hook)
+        rb = PL.compute_set(nxt["P"], comm, cfg)
+        return ra, rb
+
+    outs = run_loopback(size, fn)
+    assert torch.equal(torch.cat([o[0] for o in outs]), oracle(A, k))
+    assert torch.equal(torch.cat([o[1] for o in outs]), oracle(B, k))
