@@ -101,12 +101,13 @@ class SetStream:
             if i + 1 < n:
                 self._prefetch(i + 1, inputs[i + 1])
             info = new_info()
-            res = PL.unordered_knn(pts, self.comm, self.cfg, info, n_total=n_totals[i],
-                                   out=outputs[i] if self.direct_out else None)
-            if res.data_ptr() != outputs[i].data_ptr():
-                outputs[i].copy_(res, non_blocking=True)
-            del res
-            torch.cuda.synchronize(self.device)
+            with trace.range(f"lsknn:set {i}"):
+                res = PL.unordered_knn(pts, self.comm, self.cfg, info, n_total=n_totals[i],
+                                       out=outputs[i] if self.direct_out else None)
+                if res.data_ptr() != outputs[i].data_ptr():
+                    outputs[i].copy_(res, non_blocking=True)
+                del res
+                torch.cuda.synchronize(self.device)
             self.last_info = info
         torch.cuda.synchronize(self.device)  # the last results are in host memory
 
@@ -140,7 +141,8 @@ class SetStream:
                     nxt["P"] = PL.redistribute_set(self._dbuf[j % 2], comm, cfg, n_totals[j])
                 return redist
 
-            res = PL.compute_set(P, comm, cfg, info, hook=hook if i + 1 < n else None)
+            with trace.range(f"lsknn:set {i}"):
+                res = PL.compute_set(P, comm, cfg, info, hook=hook if i + 1 < n else None)
             self.out_stream.wait_stream(cur)
             with torch.cuda.stream(self.out_stream):
                 outputs[i].copy_(res, non_blocking=True)
