@@ -32,6 +32,7 @@ from typing import Callable, Sequence
 import torch
 
 from ..models import knn_engine as E
+from ..utils import trace
 from . import pipelines as PL
 from .comm import Comm
 
