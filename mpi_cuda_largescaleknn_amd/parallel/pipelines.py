@@ -521,10 +521,10 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
                   info: RunInfo, final_out: torch.Tensor, hook=None) -> torch.Tensor:
     """Local k-NN of every owned query + halo exchange + re-query (distributed runs).
     Returns the sorted d2; `final_out` receives the final distances (index.perm order).
-    `hook(after_stream)` (overlapped GPU path): called once the local k-NN and the halo
-    exchange are queued, before the host waits for the k-NN — independent work issued
-    there (SetStream: the next point set's redistribution) runs under the k-NN; it must
-    order its collectives after `after_stream` (the halo exchange)."""
+    `hook(after_stream) -> stream | None` (overlapped GPU path): called right after the
+    local k-NN is queued — independent work issued there (SetStream: the next point
+    set's redistribution) runs under the k-NN; the halo exchange is ordered after the
+    stream it returns."""
     stats = info.stats if cfg.collect_stats else None
     gpu = K.is_gpu(index.pts)
     if not OVERLAP_HALO or (gpu and torch.cuda.is_current_stream_capturing()):
@@ -545,6 +545,14 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
     pend: list = []
     with torch.cuda.stream(comp):
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True, deferred=pend)
+    if hook is not None:
+        # independent work under the k-NN, issued before the halo exchange (whose host
+        # syncs wait for kernels that share the CUs with the k-NN); the halo collectives
+        # follow its collectives (one communicator: never two in flight)
+        st = hook(cur)
+        if st is not None:
+            side.wait_stream(st)
+        hook = None
     with torch.cuda.stream(side):
         recv = _halo_send(index, _radius_bounds(index, cfg), comm, cfg, info, marks=False)
     cur.wait_stream(comp)
@@ -552,8 +560,6 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
     recv.record_stream(cur)
     d2.record_stream(cur)
     final_out.record_stream(comp)
-    if hook is not None:
-        hook(side)
     E.settle(pend)
     info.counts["halo_overlap"] = 1
     info.timer.mark("knn_local+halo_exchange")
@@ -785,8 +791,12 @@ def compute_set(P: Redistributed, comm: Comm, cfg: E.KnnConfig, info: RunInfo | 
     info.timer.mark("build")
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     used: list = []
-    knn_with_halo(index, comm, cfg, P.hint2, info, dist_owned,
-                  hook=(lambda after: used.append(hook(after))) if hook is not None else None)
+    def _hook(after):
+        st = hook(after)
+        used.append(st)
+        return st
+
+    knn_with_halo(index, comm, cfg, P.hint2, info, dist_owned, hook=_hook if hook is not None else None)
     if hook is not None and not used:  # (a path without the overlap point: run it here)
         used.append(hook(torch.cuda.current_stream(dev)) if K.is_gpu(dist_owned) else hook(None))
     for st in used:

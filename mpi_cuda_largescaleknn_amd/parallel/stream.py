@@ -11,11 +11,11 @@ before ~1.4 s of index build and k-NN. `SetStream` overlaps them across sets:
 * one rank: the k-NN kernel writes set i's distances straight into its pinned host
   output while it runs (pipelines.local_query), nothing to copy afterwards;
 * several ranks: set i+1's spatial redistribution (bounds, splitters, all-to-all-v of
-  the points) is issued on a fourth stream right after set i's local k-NN and halo
-  exchange are queued, so it runs under set i's k-NN (pipelines.compute_set hook; its
-  collectives are ordered after the halo exchange and before set i's result return,
-  one communicator never has two collectives in flight); set i's returned distances go
-  device -> host on a third stream under set i+1 (kept alive with record_stream).
+  the points) is issued on a fourth, high-priority stream right after set i's local k-NN
+  is queued, so it runs under set i's k-NN (pipelines.compute_set hook; set i's halo
+  exchange and result return are ordered after its collectives, one communicator never
+  has two collectives in flight); set i's returned distances go device -> host on a
+  third stream under set i+1 (kept alive with record_stream).
 
 Every set is still uploaded, redistributed (several ranks), built, queried and returned in
 full; only the order in which independent work is issued changes. On a CPU device the sets
@@ -54,7 +54,8 @@ class SetStream:
         if self.gpu:
             self.copy_stream = torch.cuda.Stream(self.device)
             self.out_stream = torch.cuda.Stream(self.device)
-            self.redist_stream = torch.cuda.Stream(self.device)
+            # high priority: its kernels get CU slots as the k-NN grid's workgroups retire
+            self.redist_stream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
         self._dbuf: list[torch.Tensor | None] = [None, None]
         self.last_info: PL.RunInfo | None = None
 
@@ -134,8 +135,8 @@ class SetStream:
             nxt: dict = {}
 
             def hook(after, j=i + 1):
-                # set j's redistribution under set i's k-NN: after the halo exchange's
-                # collectives, once set j's points are on the device
+                # set j's redistribution under set i's k-NN (issued right after the k-NN
+                # launch), once set j's points are on the device
                 redist.wait_stream(after)
                 redist.wait_stream(self.copy_stream)
                 with torch.cuda.stream(redist):
