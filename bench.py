@@ -14,7 +14,7 @@ clock: host points -> H2D -> (unordered variant) spatial redistribution + bucket
 k-NN + halo exchange + result return -> distances back in host memory. W untimed warmup
 steps, then K steps bracketed by barrier + device sync; the max over ranks is reported.
 
-Pipelined (default for the unordered halo pipeline on GPUs, --pipeline): the bench is a
+Pipelined (default for the unordered halo pipeline on GPUs from 1e7 points, --pipeline): a
 stream of point sets — two different synthetic sets alternate step by step, and while
 step i runs its k-NN on the compute stream, step i+1's points are copied host -> device
 (PCIe H2D does not compete with the VALU-bound k-NN). Every step still uploads, builds, queries and
@@ -51,6 +51,7 @@ from mpi_cuda_largescaleknn_amd.utils import trace, verify  # noqa: E402
 HEADLINE_METRIC = "Mpoints/sec kNN-distance (k=100) on 1B float3 at 1/2/4/8 MI355X"
 GEN_CHUNK = 1 << 24  # points per seeded generation chunk (global index -> seed)
 DATASET_STRIDE = 1_000_003  # seed offset of the second point set of the pipelined bench
+PIPELINE_MIN_POINTS = 10**7  # --pipeline -1: stream of sets from this many points on
 # "knn_local+halo_exchange": the overlapped form (pipelines.knn_with_halo) — the local k-NN
 # and the halo publish/filter/exchange on a side stream end at one mark
 PHASES = ["bounds", "partition", "alltoallv_points", "build", "knn_local", "knn_local+halo_exchange",
@@ -100,7 +101,7 @@ def parse():
                          "returns its whole set; the first upload is inside the timed region); "
                          "0 = one set, each step uploads then computes (on several ranks the upload "
                          "is streamed under the redistribution); -1 (default) = 1 for the unordered "
-                         "halo pipeline on GPUs")
+                         "halo pipeline on GPUs from 1e7 points")
     ap.add_argument("--verify", type=int, default=256,
                     help="sampled outputs checked by brute force after the timed region (0 = off)")
     return ap.parse_args()
@@ -156,7 +157,10 @@ def main():
     cfg = KnnConfig(k=args.k, collect_stats=args.stats)
 
     # pipelined stream of point sets (see --pipeline): two different synthetic sets alternate
-    pipelined = args.pipeline != 0 and device.type == "cuda" \
+    # (auto: from 1e7 points; below that one HIP-graph replay per set is cheaper than the
+    # eager launches of the stream: 1e6 k=8 711 vs 702 Mpts/s, profiles/r2_s3_table)
+    pipelined = (args.pipeline == 1 or (args.pipeline < 0 and n_total >= PIPELINE_MIN_POINTS)) \
+        and device.type == "cuda" \
         and args.variant == "unordered" and args.mode == "halo"
     host_sets = [make_points(n_total, rank, world, device, args.variant, d) for d in range(2 if pipelined else 1)]
     host_outs = [torch.empty(h.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda") for h in host_sets]

@@ -61,10 +61,11 @@ def test_bench_single_gpu_graph_and_eager(graph):
 
 
 @pytest.mark.gpu
-def test_bench_single_gpu_pipelined_default():
-    """The default single-GPU bench: a stream of two alternating point sets, step i+1's
+def test_bench_single_gpu_pipelined():
+    """The single-GPU bench as a stream of two alternating point sets, step i+1's
     upload under step i's k-NN; both sets' outputs of the last two steps are checked."""
-    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "3", "--warmup", "1"],
+    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "3", "--warmup", "1",
+                          "--pipeline", "1"],  # (the default turns the stream on from 1e7 points)
                          cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = _json_line(out.stdout)
@@ -162,7 +163,7 @@ def test_bench_two_gpu_ranks_pipelined_gloo():
     refuses two ranks on one device): both sets' sampled outputs exact."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--points", "400000", "--steps", "3", "--warmup", "1"]
+           "--points", "400000", "--steps", "3", "--warmup", "1", "--pipeline", "1"]
     out = subprocess.run(cmd, cwd=ROOT, env=dict(_env(), LSKNN_DIST_BACKEND="gloo"), capture_output=True,
                          text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
