@@ -14,8 +14,8 @@ clock: host points -> H2D -> (unordered variant) spatial redistribution + bucket
 k-NN + halo exchange + result return -> distances back in host memory. W untimed warmup
 steps, then K steps bracketed by barrier + device sync; the max over ranks is reported.
 
-Pipelined (default for the unordered halo pipeline on GPUs from 1e7 points, --pipeline): a
-stream of point sets — two different synthetic sets alternate step by step, and while
+Pipelined (--pipeline; default for the unordered halo pipeline on GPUs from 1e7
+points): a stream of point sets — two different synthetic sets alternate step by step, and while
 step i runs its k-NN on the compute stream, step i+1's points are copied host -> device
 (PCIe H2D does not compete with the VALU-bound k-NN). Every step still uploads, builds, queries and
 returns its whole set; the first set's upload is inside the timed region, and both sets'
