@@ -141,8 +141,28 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
+def self_launch(args) -> int | None:
+    """--gpus N without a launcher: start N local ranks of this script (the torchrun
+    contract: RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*; the reference's `mpirun -n P`,
+    README.md:31,39) before anything touches the GPU, and return the first non-zero exit
+    code (rank 0 prints the JSON line). Under a launcher its world size must equal --gpus.
+    Returns None when this process is a rank and should run the benchmark."""
+    if not LA.launcher_env():
+        if args.gpus > 1:
+            return LA.spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__), *sys.argv[1:]])
+        return None
+    _, size, _ = LA.rank_info()
+    if size != args.gpus:
+        sys.stderr.write(f"bench.py: the launcher started {size} ranks but --gpus is {args.gpus}\n")
+        return 2
+    return None
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     # a hung collective ends the job (watchdog + collective timeout) long before the
     # driver's limit; one rank per GPU (ranks beyond the device count wrap: rehearsals
     # with LSKNN_DIST_BACKEND=gloo only, RCCL refuses two ranks on one GPU); pinned
@@ -246,6 +266,7 @@ def main():
             step()
     comm.barrier()
     _sync(device)
+    ncoll0 = comm.collectives()
     t0 = time.perf_counter()
     if pipelined:
         run_steps(args.steps)
@@ -255,6 +276,8 @@ def main():
     comm.barrier()
     _sync(device)
     elapsed = time.perf_counter() - t0
+    # collective launches of the timed steps (the closing barrier excluded)
+    coll_per_step = (comm.collectives() - ncoll0 - (1 if comm.distributed else 0)) / max(1, args.steps)
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.allreduce_(t, "max")
     elapsed = float(t.item())
@@ -316,6 +339,8 @@ def main():
                 "k": args.k,
                 "comm": (getattr(getattr(comm, "inner", comm), "backend", "single")
                          if comm.distributed else "single"),
+                "ranks": world,
+                "collectives_per_step": round(coll_per_step, 2),
                 "hip_graph": graph is not None,
                 "pipelined": pipelined,
                 "heavy_cells_unrefined": heavy_unrefined,

@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 4  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 5  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -85,6 +85,17 @@ class KnnArgs(C.Structure):
         ("fail_cap", i64),
         ("debug_fail_mod", C.c_int32),
         ("pad1", C.c_int32),
+    ]
+
+
+class GridView(C.Structure):
+    _fields_ = [
+        ("cells", vp),
+        ("subs", vp),
+        ("box", vp),
+        ("inf4", vp),
+        ("level", C.c_int32),
+        ("pad", C.c_int32),
     ]
 
 
@@ -153,6 +164,10 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_tree_set_radii_ub": ([vp, vp, i64, i32, vp], i32),
         "lsk_hip_knn_exact": ([C.POINTER(KnnArgs), vp, vp, i64, vp], i32),
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
+        "lsk_hip_knn_grid": ([C.POINTER(KnnArgs), C.POINTER(GridView), vp], i32),
+        "lsk_hip_grid_build": ([vp, i64, vp, i32, vp, vp, vp], i32),
+        "lsk_hip_key_levels": ([vp, i64, vp, vp], i32),
+        "lsk_hip_grid_sq": ([vp, i64, vp, vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),
         "lsk_hip_flag_query_groups": ([vp, vp, i64, vp, C.c_int32, i64, vp, vp], i32),
         "lsk_hip_flag_groups_inverse": ([vp, i64, vp, C.c_int32, i64, vp, vp], i32),

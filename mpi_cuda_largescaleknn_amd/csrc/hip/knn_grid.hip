@@ -1,0 +1,849 @@
+// k-th-NN distance selection with a cell-grid candidate source (the near-uniform fast path).
+//
+// Same contract and selection algorithm as knn_rows.hip (two-pass radix select on the
+// float bits of d² with a per-lane 16-bit LDS histogram, LDS collect pool and a per-lane
+// (k - below)-max-heap, exact on every input through the failure list + knn_exact.hip
+// backstop; reference runQuery / extractFinalResult, unorderedDataVariant.cu:75-103). What
+// differs is where the candidates come from and how they are broadcast:
+//
+//  * the Hilbert-sorted points are indexed by an octree grid at two levels: every cell of
+//    level `lc` and every one of its 8 sub-cells (level lc+1) is a contiguous run of the
+//    sorted array (an aligned block of Hilbert keys), stored as (start, end) pairs in
+//    Morton order of the cell coordinates (the 8 sub-cells of a cell are 8 consecutive
+//    entries). Built in one pass over the sorted points (grid_build_kernel);
+//  * a wave owns 64 curve-consecutive queries. A pass enumerates the cells around the
+//    wave's query box ARITHMETICALLY (cell coordinates from the quantised box ± the
+//    current radius; no pointer chasing, no priority queue): lane j tests cell j of the
+//    range against the box, the needed cells are taken in ballot order, the cells
+//    holding the queries first (their candidates shrink the histogram ranges early);
+//  * per cell, lanes 0-7 test its 8 sub-cells; a fully needed cell is one contiguous
+//    segment, otherwise every needed sub-cell is one;
+//  * a segment's points are read with SCALAR loads (wave-uniform addresses through the
+//    constant address space): the candidates arrive in SGPRs and every VALU op of the
+//    canonical d² takes them as an operand — 6 VALU per candidate and lane, no
+//    broadcast, no per-row queues or logs. The per-lane bound only shrinks during a pass,
+//    and the cull radius follows it cell by cell.
+//
+// Every cull is conservative: cell boxes are the quantisation intervals widened by a
+// few ulps of the cube, the radius is inflated by 2^-16 (relative) over the largest lane
+// bound, so a skipped point always has canonical d² >= every lane's bound.
+#include "dev.h"
+
+namespace {
+
+using lsk::bitsf;
+using lsk::fbits;
+
+#ifndef LSK_GRID_MINW
+#define LSK_GRID_MINW 7  // waves per SIMD the register budget is sized for
+#endif
+#ifndef LSK_GRID_WPB
+#define LSK_GRID_WPB 2
+#endif
+constexpr int kWPB = LSK_GRID_WPB;
+constexpr int kThreads = kWPB * lsk::kWave;
+constexpr int kBins = 40;                 // 16-bit bins, two per LDS dword (as knn_rows)
+constexpr int kPool = kBins / 2 * 64;     // dwords per wave: histogram, or collect pool
+#ifndef LSK_GRID_TOPBINS
+#define LSK_GRID_TOPBINS 12
+#endif
+constexpr int kTopBins = LSK_GRID_TOPBINS;  // first range tops out 1.5 octaves above the estimate
+constexpr uint32_t kLogBins = 5;          // floor(log2(kBins))
+constexpr uint32_t kShift0 = 20;          // 1/8 octave of d² per bin
+constexpr uint32_t kMaxPasses = 24;
+constexpr uint32_t kUnknown = 0xffffffffu;
+constexpr uint32_t kNaNBits = 0x7fc00000u;
+constexpr float kEstCalib = 0.8f;
+
+enum : uint32_t { ST_HIST = 0, ST_READY = 1, ST_DONE = 2 };
+enum { MODE_HIST = 0, MODE_COLLECT = 1 };
+enum : uint32_t {
+  QS_OVERFLOW = 1, QS_UNDERFLOW = 2, QS_REFINE = 4, QS_COLLECTED = 16, QS_DONE_BAND1 = 32,
+  QS_DONE_CUT = 64, QS_LIMIT = 256, QS_MISMATCH = 512, QS_HINT = 1024, QS_BINOVF = 2048,
+  QS_FAIL = 4096
+};
+
+struct Lane {
+  float qx, qy, qz;
+  uint32_t state;
+  uint32_t lo_b, hi_b, shift;  // histogram range; lo_b holds the answer once DONE
+  int32_t bin_hi;
+  uint32_t c_hi;     // values < hi_b counted this pass (exact, 32-bit)
+  uint32_t c_base;   // exact count below lo_b, or kUnknown (READY: count below the band)
+  uint32_t nudf;
+  uint32_t band_lo, band_w, bc;
+  uint32_t coff, ccnt;
+};
+
+__device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift, uint32_t top_limit,
+                                          uint32_t c_base) {
+  s.lo_b = lo_b;
+  s.c_base = lo_b == 0 ? 0u : c_base;
+  s.shift = shift;
+  const uint64_t top = (uint64_t)lo_b + ((uint64_t)kBins << shift);
+  const uint64_t hi = top < (uint64_t)top_limit ? top : (uint64_t)top_limit;
+  s.hi_b = (uint32_t)hi;
+  s.bin_hi = hi > lo_b ? (int32_t)((hi - lo_b + ((1ull << shift) - 1)) >> shift) : 0;
+  s.c_hi = 0;
+}
+
+__device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
+  return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
+}
+
+__device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *pool, int lane) {
+  return s.bin_hi > 0 ? hist_read(pool, (uint32_t)s.bin_hi - 1u, lane) : s.c_hi;
+}
+
+__device__ __forceinline__ void underflow_restart(Lane &s) {
+  const uint32_t topb = s.hi_b;
+  if (s.nudf == 0 && topb > ((uint32_t)kBins << kShift0)) {
+    set_range(s, topb - ((uint32_t)kBins << kShift0), kShift0, topb, kUnknown);
+  } else {
+    uint32_t sh = 0;
+    while (((uint64_t)kBins << sh) < (uint64_t)topb) sh++;
+    set_range(s, 0u, sh, topb, 0u);
+  }
+  s.nudf++;
+}
+
+// Drop top bins while at least k counted values stay below: the lane's bound shrinks.
+__device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
+  while (s.bin_hi > 0) {
+    const uint32_t top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
+    if (s.c_hi - top < k) break;
+    s.c_hi -= top;
+    s.bin_hi--;
+    s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
+  }
+  // k exact zeros: the k-th is 0 and nothing can be closer (knn_rows zero probe)
+  if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
+}
+
+// 16-bit bin checksum (see knn_rows.hip hist_consistent): the counter sum over [0, bin_hi)
+// equals c_hi iff no counter wrapped.
+__device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *pool, int lane) {
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kBins / 2; j++) {
+    const uint32_t w = pool[j * lsk::kWave + lane];
+    sum += (2 * j < s.bin_hi ? (w & 0xffffu) : 0u) + (2 * j + 1 < s.bin_hi ? (w >> 16) : 0u);
+  }
+  return sum == s.c_hi;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// wave max of non-negative floats (DPP inside rows, scalar combine of the 4 rows)
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 0);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 32);
+  const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 48);
+  return __uint_as_float(max(max(a, b), max(c, d)));
+}
+
+__device__ __forceinline__ float bcast64(float v, uint32_t j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
+}
+
+// 8-NN among the wave's own 64 queries, scaled to k (knn_rows own_group_estimate).
+__device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k,
+                                                     bool &dup) {
+  constexpr int M = 8;
+  float best[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) best[i] = __builtin_inff();
+  for (uint32_t j0 = 0; j0 < nvalid; j0 += 8) {
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const uint32_t j = j0 + (uint32_t)t;
+      float v = lsk::dist2(s.qx - bcast64(s.qx, j), s.qy - bcast64(s.qy, j), s.qz - bcast64(s.qz, j));
+      v = (j < nvalid) ? v : __builtin_inff();
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const float lo = fminf(best[i], v);
+        v = fmaxf(best[i], v);
+        best[i] = lo;
+      }
+    }
+  }
+  dup = best[1] == 0.f;
+  const uint32_t m0 = k < (uint32_t)M ? k : (uint32_t)M;
+  float dm = best[0];
+#pragma unroll
+  for (int i = 1; i < M; i++) dm = (i + 1 == (int)m0) ? best[i] : dm;
+  return dm * cbrtf(((float)k / (float)m0) * ((float)k / (float)m0));
+}
+
+__device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
+  const uint32_t v = h[i];
+  for (;;) {
+    uint32_t l = 2 * i + 1, r = l + 1, c = i;
+    uint32_t cv = v;
+    if (l < m && h[l] > cv) { c = l; cv = h[l]; }
+    if (r < m && h[r] > cv) { c = r; cv = h[r]; }
+    if (c == i) break;
+    h[i] = cv;
+    i = c;
+  }
+  h[i] = v;
+}
+
+// Wave-uniform grid context.
+struct GridCtx {
+  const float *pts;        // sorted points (packed float3, padded)
+  const float *inf4;       // 4 x +inf (tail padding of a candidate batch)
+  const uint32_t *cells;   // level-lc (start, end) pairs, Morton index
+  const uint32_t *subs;    // level-lc+1 pairs
+  float ox, oy, oz;        // cube origin
+  float scale;             // 1024 / extent (the sort keys' quantisation)
+  float step;              // extent / 1024: one level-10 quantum
+  float eps;               // absolute slack of cell boundaries and the cull radius
+  uint32_t lc;             // cell level
+  float wlx, wly, wlz, whx, why, whz;  // box of the wave's queries
+  uint32_t *pool;
+  int lane;
+  uint32_t k;
+  uint32_t evals, cells_n, segs;
+};
+
+// Cell coordinate at level l (monotone in v: a point with coordinate v' <= v never lies in
+// a later cell — the same float ops as the sort keys, common.h morton_quant).
+__device__ __forceinline__ uint32_t cell_of(float v, float o, float scale, uint32_t sh) {
+  return lsk::morton_quant(v, o, scale) >> sh;
+}
+
+// Conservative [lo, hi] of cell c (level-10 quanta [c << sh, (c+1) << sh)) on one axis.
+__device__ __forceinline__ void cell_span(const GridCtx &G, float o, uint32_t c, uint32_t sh, uint32_t last,
+                                          float &lo, float &hi) {
+  lo = c == 0 ? -__builtin_inff() : o + (float)(c << sh) * G.step - G.eps;
+  hi = c >= last ? __builtin_inff() : o + (float)((c + 1u) << sh) * G.step + G.eps;
+}
+
+__device__ __forceinline__ float gap1(float lo, float hi, float wl, float wh) {
+  return fmaxf(0.f, fmaxf(lo - wh, wl - hi));
+}
+
+// gap² between the cell (x, y, z) of level (10 - sh) and the wave's query box
+__device__ __forceinline__ float cell_gap2(const GridCtx &G, uint32_t x, uint32_t y, uint32_t z, uint32_t sh) {
+  const uint32_t last = (1023u >> sh);
+  float lx, hx, ly, hy, lz, hz;
+  cell_span(G, G.ox, x, sh, last, lx, hx);
+  cell_span(G, G.oy, y, sh, last, ly, hy);
+  cell_span(G, G.oz, z, sh, last, lz, hz);
+  return lsk::dist2(gap1(lx, hx, G.wlx, G.whx), gap1(ly, hy, G.wly, G.why), gap1(lz, hz, G.wlz, G.whz));
+}
+
+// Per-lane bound of the current pass (HIST: range top; COLLECT: band top; else 0).
+template <int MODE>
+__device__ __forceinline__ float lane_bound(const Lane &s) {
+  if (MODE == MODE_HIST) return s.state == ST_HIST ? bitsf(s.hi_b) : 0.f;
+  return s.band_w ? bitsf(s.band_lo + s.band_w) : 0.f;
+}
+
+// Squared cull radius over the wave: every lane's bound, inflated so that a point whose
+// true distance to the query box is at least this radius has canonical d² >= the bound
+// (relative 2^-16 covers the rounding of d² and of the gap arithmetic; eps covers the
+// absolute rounding of coordinates).
+template <int MODE>
+__device__ __forceinline__ float cull_r2(const Lane &s, const GridCtx &G) {
+  const float b = wave_max_nonneg(lane_bound<MODE>(s));
+  if (fbits(b) == 0u) return 0.f;  // (bits: a denormal bound is still a bound)
+  const float r = sqrtf(b) * (1.f + 0x1p-16f) + G.eps;
+  return r * r;
+}
+
+template <int MODE>
+__device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3,
+                                        uint32_t *pool, int lane) {
+  if (MODE == MODE_HIST) {
+    const uint32_t um = min(min(u0, u1), min(u2, u3));
+    if (!__ballot(um < s.hi_b)) return;
+    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
+    const uint32_t u[4] = {u0, u1, u2, u3};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const uint32_t v = u[t];
+      if (v < hb) {
+        const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
+        const uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
+        const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
+        atomicAdd(&pool[dw * lsk::kWave + lane], __umul24(half, 0xffffu) + 1u);
+        s.c_hi++;
+      }
+    }
+  } else {
+    const uint32_t bl = s.band_lo, bw = s.band_w;
+    const bool any = (u0 - bl < bw) || (u1 - bl < bw) || (u2 - bl < bw) || (u3 - bl < bw);
+    if (!__ballot(any)) return;
+    const uint32_t u[4] = {u0, u1, u2, u3};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      if (u[t] - bl < bw) {
+        if (s.ccnt < s.bc) pool[s.coff + s.ccnt] = u[t];
+        s.ccnt++;
+      }
+    }
+  }
+}
+
+// Points [i0, i1) of the sorted array, 4 per batch through scalar loads, software
+// pipelined: the wait for batch i (lgkmcnt(0): scalar loads may return out of order, so
+// only an empty queue proves a batch complete) comes BEFORE batch i+1's loads are issued,
+// which then fly while batch i is computed. Reads past i1 stay inside the array's
+// 64-point readable pad (i < i1 <= n).
+struct Batch {
+  float x0, y0, z0, x1, y1, z1, x2, y2, z2, x3, y3, z3;
+};
+// 4 consecutive points: 12 dwords in two scalar loads (x8 + x4)
+__device__ __forceinline__ Batch load_batch(lsk::cfloat_p P, uint32_t i) {
+  const lsk::cfloat_p p = P + 3ull * (uint64_t)i;
+  return Batch{p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9], p[10], p[11]};
+}
+constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0) (vmcnt / expcnt untouched)
+
+template <int MODE>
+__device__ __forceinline__ void eval4(Lane &s, GridCtx &G, const Batch &b) {
+  const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
+  const uint32_t u1 = fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1));
+  const uint32_t u2 = fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2));
+  const uint32_t u3 = fbits(lsk::dist2(s.qx - b.x3, s.qy - b.y3, s.qz - b.z3));
+  update4<MODE>(s, u0, u1, u2, u3, G.pool, G.lane);
+}
+
+// Unrolled by two with separate A / B batch registers: a loop-carried copy of the batch
+// would make the compiler wait for the prefetch right after issuing it.
+template <int MODE>
+__device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0, uint32_t i1) {
+  const lsk::cfloat_p P = lsk::as_const(G.pts);
+  i0 = lsk::uniform(i0);
+  i1 = lsk::uniform(i1);
+  uint32_t i = i0;
+  Batch A = load_batch(P, i);
+  for (;;) {  // A holds batch i (in flight)
+    if (i + 4u > i1) break;
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    Batch B = load_batch(P, i + 4u < i1 ? i + 4u : i);
+    __builtin_amdgcn_sched_barrier(0);
+    eval4<MODE>(s, G, A);
+    i += 4u;
+    if (i + 4u > i1) {
+      A = B;  // (tail: once per segment)
+      break;
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    A = load_batch(P, i + 4u < i1 ? i + 4u : i);
+    __builtin_amdgcn_sched_barrier(0);
+    eval4<MODE>(s, G, B);
+    i += 4u;
+  }
+  if (i < i1) {  // 1-3 tail points (already loaded): slots past the end count nowhere
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    const uint32_t left = i1 - i;
+    const Batch &b = A;
+    const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
+    const uint32_t u1 = left > 1u ? fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1)) : ~0u;
+    const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
+    update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane);
+  }
+  G.evals += (i1 - i0 + 3u) & ~3u;
+  G.segs++;
+}
+
+template <int MODE>
+__device__ __forceinline__ void shrink_all(Lane &s, GridCtx &G) {
+  if (MODE == MODE_HIST && __ballot(s.state == ST_HIST && s.c_hi >= G.k)) {
+    if (s.state == ST_HIST && s.c_hi >= G.k) hist_shrink(s, G.pool, G.lane, G.k);
+  }
+}
+
+// Table entries of one level-lc cell, fetched ahead of use (vector loads: their counter
+// retires in order, so the wait lands at the first use, one cell later): lanes 0-7 hold
+// sub-cell j's (start, end), every other lane the cell's own.
+struct CellLoad {
+  uint32_t x, y, z;
+  uint32_t a, e;  // per lane
+};
+__device__ __forceinline__ CellLoad fetch_cell(const GridCtx &G, uint32_t x, uint32_t y, uint32_t z) {
+  const uint32_t mc = lsk::morton3(x, y, z);
+  const uint32_t *src = G.lane < 8 ? G.subs + 2u * (8u * mc + (uint32_t)G.lane) : G.cells + 2u * mc;
+  const uint2 v = *(const uint2 *)src;
+  return CellLoad{x, y, z, v.x, v.y};
+}
+
+// One level-lc cell: lanes 0-7 test its 8 sub-cells against the wave box; a fully needed
+// cell is one segment.
+template <int MODE>
+__device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad &c, float r2) {
+  const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)c.a, 8);
+  const uint32_t ce = (uint32_t)__builtin_amdgcn_readlane((int)c.e, 8);
+  if (cs >= ce) return;
+  G.cells_n++;
+  const uint32_t j = (uint32_t)G.lane & 7u;
+  const uint32_t sh = 10u - (G.lc + 1u);
+  const float g2 = cell_gap2(G, 2u * c.x + ((j >> 2) & 1u), 2u * c.y + ((j >> 1) & 1u), 2u * c.z + (j & 1u), sh);
+  const bool sub = G.lane < 8 && c.e > c.a;
+  const uint32_t nonempty = (uint32_t)__ballot(sub);
+  const uint32_t need = (uint32_t)__ballot(sub && g2 <= r2);
+  if (need == 0u) return;
+  if (need == nonempty) {
+    process_segment<MODE>(s, G, cs, ce);
+  } else {
+    uint32_t m = need;
+    while (m) {
+      const int b = __builtin_ctz(m);
+      m &= m - 1u;
+      process_segment<MODE>(s, G, (uint32_t)__builtin_amdgcn_readlane((int)c.a, b),
+                            (uint32_t)__builtin_amdgcn_readlane((int)c.e, b));
+    }
+  }
+  shrink_all<MODE>(s, G);
+}
+
+// One pass over every cell within the cull radius of the wave's query box (cells that
+// hold the queries first). The radius is re-read after every cell (bounds only shrink).
+// Cells are enumerated in 4x4x4 blocks, lane l taking cell (l & 3, (l >> 2) & 3, l >> 4) of
+// the block (no integer division). A range of more than kMaxCells cells (a bound far above
+// the local spacing: k beyond the local point count, or an estimate far off) is served by
+// one scan of all points when the tree is small, else the wave hands its unresolved
+// queries to the exact backstop (returns false).
+constexpr uint32_t kMaxCells = 4096;
+constexpr uint32_t kScanAll = 1u << 16;
+
+template <int MODE>
+__device__ bool grid_pass(Lane &s, GridCtx &G, uint32_t n) {
+  float r2 = cull_r2<MODE>(s, G);
+  if (fbits(r2) == 0u) return true;
+  const uint32_t sh = 10u - G.lc;
+  const float r = sqrtf(r2);
+  const uint32_t x0 = cell_of(G.wlx - r, G.ox, G.scale, sh), x1 = cell_of(G.whx + r, G.ox, G.scale, sh);
+  const uint32_t y0 = cell_of(G.wly - r, G.oy, G.scale, sh), y1 = cell_of(G.why + r, G.oy, G.scale, sh);
+  const uint32_t z0 = cell_of(G.wlz - r, G.oz, G.scale, sh), z1 = cell_of(G.whz + r, G.oz, G.scale, sh);
+  if ((uint64_t)(x1 - x0 + 1u) * (y1 - y0 + 1u) * (z1 - z0 + 1u) > kMaxCells) {
+    if (n > kScanAll) return false;
+    process_segment<MODE>(s, G, 0u, n);
+    shrink_all<MODE>(s, G);
+    return true;
+  }
+  const uint32_t bx0 = cell_of(G.wlx, G.ox, G.scale, sh), bx1 = cell_of(G.whx, G.ox, G.scale, sh);
+  const uint32_t by0 = cell_of(G.wly, G.oy, G.scale, sh), by1 = cell_of(G.why, G.oy, G.scale, sh);
+  const uint32_t bz0 = cell_of(G.wlz, G.oz, G.scale, sh), bz1 = cell_of(G.whz, G.oz, G.scale, sh);
+  const uint32_t lx = (uint32_t)G.lane & 3u, ly = ((uint32_t)G.lane >> 2) & 3u, lz = (uint32_t)G.lane >> 4;
+  CellLoad pend{0u, 0u, 0u, 0u, 0u};
+  bool have = false;
+  for (int phase = 0; phase < 2; phase++) {
+    const uint32_t ax = phase ? x0 : bx0, ay = phase ? y0 : by0, az = phase ? z0 : bz0;
+    const uint32_t ex = phase ? x1 : bx1, ey = phase ? y1 : by1, ez = phase ? z1 : bz1;
+    for (uint32_t oz = az; oz <= ez; oz += 4u)
+      for (uint32_t oy = ay; oy <= ey; oy += 4u)
+        for (uint32_t ox = ax; ox <= ex; ox += 4u) {
+          const uint32_t cx = ox + lx, cy = oy + ly, cz = oz + lz;
+          const bool core = cx >= bx0 && cx <= bx1 && cy >= by0 && cy <= by1 && cz >= bz0 && cz <= bz1;
+          const bool valid = cx <= ex && cy <= ey && cz <= ez && (phase == 0 || !core);
+          const float g2 = valid ? cell_gap2(G, cx, cy, cz, sh) : __builtin_inff();
+          uint64_t m = __ballot(g2 <= r2);
+          while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const float gb = bcast64(g2, (uint32_t)b);
+            if (!(gb <= r2)) continue;  // the radius shrank since the test
+            // fetch this cell's entries, then process the one fetched before it
+            const CellLoad c = fetch_cell(G, ox + ((uint32_t)b & 3u), oy + (((uint32_t)b >> 2) & 3u),
+                                          oz + ((uint32_t)b >> 4));
+            if (have) {
+              process_cell<MODE>(s, G, pend, r2);
+              if (MODE == MODE_HIST) r2 = cull_r2<MODE>(s, G);
+              if (fbits(r2) == 0u) return true;
+            }
+            pend = c;
+            have = true;
+          }
+        }
+  }
+  if (have) process_cell<MODE>(s, G, pend, r2);
+  return true;
+}
+
+__global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
+  __shared__ uint32_t lds[kWPB][kPool];
+  const int wid = threadIdx.x >> 6;
+  const int lane = lsk::lane_id();
+  const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
+  const uint64_t wave = (uint64_t)blk * kWPB + wid;
+  const uint64_t ngroups = (uint64_t)((A.nq + 63) / 64);
+  if (wave >= ngroups) return;
+  const int64_t q0 = (int64_t)wave * lsk::kBucket;
+  const int64_t qi = q0 + lane;
+  const bool valid = qi < A.nq;
+  const uint32_t nvalid = (uint32_t)((A.nq - q0) < lsk::kBucket ? (A.nq - q0) : lsk::kBucket);
+  const uint32_t k = (uint32_t)A.k;
+  uint32_t *pool = lds[wid];
+
+  GridCtx G;
+  G.pts = A.tree[0].pts;
+  G.inf4 = V.inf4;
+  G.cells = V.cells;
+  G.subs = V.subs;
+  {
+    const lsk::cfloat_p bx = lsk::as_const(V.box);
+    G.ox = bx[0];
+    G.oy = bx[1];
+    G.oz = bx[2];
+    G.scale = bx[6];
+    const float ext = bx[7];
+    G.step = ext * (1.f / 1024.f);
+    const float mag = fmaxf(fmaxf(fabsf(G.ox), fabsf(G.oy)), fmaxf(fabsf(G.oz), 0.f)) + ext;
+    G.eps = mag * 0x1p-19f;
+  }
+  G.lc = (uint32_t)V.level;
+  G.pool = pool;
+  G.lane = lane;
+  G.k = k;
+  G.evals = G.cells_n = G.segs = 0;
+
+  Lane s;
+  s.qx = valid ? A.qpts[3 * qi] : 0.f;
+  s.qy = valid ? A.qpts[3 * qi + 1] : 0.f;
+  s.qz = valid ? A.qpts[3 * qi + 2] : 0.f;
+  uint32_t qs = 0;
+  const float inf = __builtin_inff();
+  G.wlx = lsk::wave_min(valid ? s.qx : inf);
+  G.whx = lsk::wave_max(valid ? s.qx : -inf);
+  G.wly = lsk::wave_min(valid ? s.qy : inf);
+  G.why = lsk::wave_max(valid ? s.qy : -inf);
+  G.wlz = lsk::wave_min(valid ? s.qz : inf);
+  G.whz = lsk::wave_max(valid ? s.qz : -inf);
+
+  bool dup;
+  float r_est2 = own_group_estimate(s, nvalid, k, dup);
+  if (valid && !dup) {
+    const int64_t nb = lane == 0 ? qi - 1 : (lane == (int)nvalid - 1 ? qi + 1 : -1);
+    if (nb >= 0 && nb < A.nq)
+      dup = A.qpts[3 * nb] == s.qx && A.qpts[3 * nb + 1] == s.qy && A.qpts[3 * nb + 2] == s.qz;
+  }
+  const bool zero_est = valid && (dup || r_est2 == 0.f);
+  {
+    const bool ok = valid && r_est2 > 0.f && r_est2 < inf;
+    const uint32_t kq = max(1u, nvalid / 4u);
+    const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
+    if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
+    const uint32_t mb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, max(1u, nvalid / 2u));
+    if (ok && mb < lsk::kInfBits) r_est2 = sqrtf(r_est2 * bitsf(mb)) * kEstCalib;
+  }
+  if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
+    r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
+    qs |= QS_HINT;
+  }
+  if (!(r_est2 > 0.f) || !(r_est2 < inf)) r_est2 = 1.f;
+
+  const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
+  const uint32_t cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
+  s.band_lo = s.band_w = s.bc = s.coff = s.ccnt = 0;
+  s.lo_b = s.hi_b = s.shift = s.c_hi = 0;
+  s.bin_hi = 0;
+  s.c_base = 0;
+  s.nudf = 0;
+
+  uint32_t hist_passes = 0, limit = 0;
+  if (!valid || A.tree[0].n < (int64_t)k) {
+    s.state = ST_DONE;
+    s.hi_b = 0;
+    s.lo_b = cut_b;
+    qs |= QS_DONE_CUT;
+  } else {
+    s.state = ST_HIST;
+    const uint32_t est_b = fbits(r_est2);
+    const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;
+    const uint32_t lo0 = est_b > off ? est_b - off : 0u;
+    if (zero_est) {
+      set_range(s, 0u, 0u, cut_lim, kUnknown);
+      s.band_lo = lo0;
+      s.band_w = 1u;
+    } else {
+      set_range(s, lo0, kShift0, cut_lim, kUnknown);
+    }
+  }
+
+  uint32_t pool_off = 0;
+  uint32_t passes = 0;
+  bool gfail = false;
+  const uint32_t ntree = (uint32_t)A.tree[0].n;
+  for (;;) {
+    while (__ballot(s.state == ST_HIST)) {
+      if (++passes > kMaxPasses) {
+        limit = 1;
+        if (s.state != ST_DONE) {
+          s.state = ST_DONE;
+          s.lo_b = kNaNBits;
+          qs |= QS_LIMIT | QS_FAIL;
+        }
+        break;
+      }
+      hist_passes++;
+      if (s.state != ST_HIST) {
+        s.hi_b = 0;
+        s.c_hi = 0;
+        s.bin_hi = 0;
+      }
+#pragma unroll 4
+      for (int j = 0; j < kPool / lsk::kWave; j++) pool[j * lsk::kWave + lane] = 0u;
+      if (!grid_pass<MODE_HIST>(s, G, ntree)) {
+        gfail = true;
+        break;
+      }
+      bool ovf = false;
+      if (s.state == ST_HIST && !hist_consistent(s, pool, lane)) {
+        s.state = ST_DONE;
+        s.lo_b = kNaNBits;
+        qs |= QS_BINOVF | QS_FAIL;
+      }
+      if (s.state == ST_HIST) {
+        const uint32_t top = top_count(s, pool, lane);
+        if (s.c_hi < k) {
+          if (s.hi_b >= cut_lim) {
+            s.state = ST_DONE;
+            s.lo_b = cut_b;
+            qs |= QS_DONE_CUT;
+          } else {
+            ovf = true;
+            qs |= QS_OVERFLOW;
+            if (s.band_w != 0u && s.band_lo > s.hi_b) {
+              set_range(s, s.band_lo, kShift0, cut_lim, kUnknown);  // failed zero probe
+            } else {
+              set_range(s, s.hi_b, kShift0, cut_lim, s.c_hi);
+            }
+            s.band_lo = s.band_w = 0u;
+          }
+        } else if (s.bin_hi <= 1 && s.c_base == kUnknown) {
+          qs |= QS_UNDERFLOW;
+          underflow_restart(s);
+        } else {
+          const uint32_t below = s.bin_hi == 1 ? s.c_base : s.c_hi - top;
+          const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
+          const uint32_t bw = s.hi_b - bl;
+          if (bw <= 1u) {
+            s.state = ST_DONE;
+            s.lo_b = bl;
+            qs |= QS_DONE_BAND1;
+          } else {
+            s.state = ST_READY;
+            s.band_lo = bl;
+            s.band_w = bw;
+            s.c_base = below;
+            s.bc = s.c_hi - below;
+          }
+        }
+      }
+      (void)ovf;
+    }
+    if (limit || gfail) break;
+    const uint32_t need = s.state == ST_READY ? s.bc : 0u;
+    uint32_t x = need;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    const uint32_t total = __shfl(x, 63);
+    pool_off = x - need;
+    if (total <= (uint32_t)kPool) break;
+    if (s.state == ST_READY && s.bc > (uint32_t)(kPool / lsk::kWave)) {
+      qs |= QS_REFINE;
+      const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;
+      set_range(s, s.band_lo, sh, s.band_lo + s.band_w, s.c_base);
+      s.band_lo = s.band_w = 0;
+      s.state = ST_HIST;
+    }
+  }
+
+  if (!limit && !gfail && __ballot(s.state == ST_READY)) {
+    if (s.state != ST_READY) s.band_lo = s.band_w = 0;
+    s.coff = pool_off;
+    s.ccnt = 0;
+    if (!grid_pass<MODE_COLLECT>(s, G, ntree)) gfail = true;
+    if (!gfail && s.state == ST_READY) {
+      qs |= QS_COLLECTED;
+      if (s.ccnt != s.bc) qs |= QS_MISMATCH | QS_FAIL;
+      uint32_t *h = pool + s.coff;
+      const uint32_t c = min(s.ccnt, s.bc), m = k - s.c_base;
+      if (!(qs & QS_FAIL) && m >= 1 && m <= c) {
+        for (int i = (int)(m / 2) - 1; i >= 0; i--) heap_sift(h, (uint32_t)i, m);
+        for (uint32_t i = m; i < c; i++) {
+          const uint32_t v = h[i];
+          if (v < h[0]) {
+            h[0] = v;
+            heap_sift(h, 0, m);
+          }
+        }
+        s.lo_b = h[0];
+      } else {
+        qs |= QS_MISMATCH | QS_FAIL;
+        s.lo_b = kNaNBits;
+      }
+    }
+  }
+
+  // a pass the grid could not serve: every unresolved query goes to the backstop
+  if (gfail && s.state != ST_DONE) qs |= QS_FAIL;
+  if (A.debug_fail_mod > 0 && qi % A.debug_fail_mod == 0) qs |= QS_FAIL;
+  const bool failed = valid && (qs & QS_FAIL);
+  if (failed) s.lo_b = kNaNBits;
+  if (A.fail_count) {
+    const uint64_t fm = __ballot(failed);
+    if (fm) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(A.fail_count, (uint32_t)__popcll(fm));
+      base = lsk::uniform(base);
+      const uint64_t slot = (uint64_t)base + (uint64_t)__popcll(fm & ((1ull << lane) - 1ull));
+      if (failed && slot < (uint64_t)A.fail_cap) A.fail_list[slot] = (uint32_t)qi;
+    }
+  }
+  if (valid) {
+    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.lo_b));
+    if (A.out_d2) A.out_d2[qi] = bitsf(s.lo_b);
+    if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
+  }
+  if (A.stats) {
+    auto cnt = [&](uint32_t bit) { return (unsigned long long)__popcll(__ballot(valid && (qs & bit))); };
+    const unsigned long long c_ovf = cnt(QS_OVERFLOW), c_udf = cnt(QS_UNDERFLOW), c_ref = cnt(QS_REFINE),
+                             c_mm = cnt(QS_MISMATCH), c_hint = cnt(QS_HINT), c_fail = cnt(QS_FAIL),
+                             c_bovf = cnt(QS_BINOVF);
+    if (lane == 0) {
+      atomicAdd(&A.stats[0], (unsigned long long)G.evals);  // candidates per lane
+      atomicAdd(&A.stats[1], (unsigned long long)G.cells_n);
+      atomicAdd(&A.stats[2], (unsigned long long)G.segs);
+      atomicAdd(&A.stats[3], (unsigned long long)hist_passes);
+      atomicAdd(&A.stats[4], c_ovf);
+      atomicAdd(&A.stats[5], c_udf);
+      atomicAdd(&A.stats[6], c_ref);
+      atomicAdd(&A.stats[7], c_mm);
+      atomicAdd(&A.stats[8], (unsigned long long)limit);
+      atomicAdd(&A.stats[10], 1ull);
+      atomicAdd(&A.stats[11], c_hint);
+      atomicAdd(&A.stats[26], c_fail);
+      atomicAdd(&A.stats[27], c_bovf);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ grid build
+__device__ __forceinline__ uint32_t sub_morton(const float *p, float ox, float oy, float oz, float s, uint32_t sh) {
+  return lsk::morton3(lsk::morton_quant(p[0], ox, s) >> sh, lsk::morton_quant(p[1], oy, s) >> sh,
+                      lsk::morton_quant(p[2], oz, s) >> sh);
+}
+
+// Run boundaries of the level-(lc+1) sub-cells and level-lc cells along the sorted points.
+__global__ __launch_bounds__(256) void grid_build_kernel(const float *__restrict__ pts, int64_t n,
+                                                         const float *__restrict__ box, uint32_t ls,
+                                                         uint32_t *__restrict__ cells, uint32_t *__restrict__ subs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float ox = box[0], oy = box[1], oz = box[2], s = box[6];
+  const uint32_t sh = 10u - ls;
+  const uint32_t m = sub_morton(pts + 3 * i, ox, oy, oz, s, sh);
+  const uint32_t mp = i > 0 ? sub_morton(pts + 3 * (i - 1), ox, oy, oz, s, sh) : ~0u;
+  const uint32_t mn = i + 1 < n ? sub_morton(pts + 3 * (i + 1), ox, oy, oz, s, sh) : ~0u;
+  if (mp != m) subs[2u * m] = (uint32_t)i;
+  if (mn != m) subs[2u * m + 1u] = (uint32_t)(i + 1);
+  const uint32_t c = m >> 3;
+  if (i == 0 || (mp >> 3) != c) cells[2u * c] = (uint32_t)i;
+  if (i + 1 == n || (mn >> 3) != c) cells[2u * c + 1u] = (uint32_t)(i + 1);
+}
+
+// counts[l] += number of i in [1, n) whose key prefix at level l (top 3l bits of the
+// 30-bit key) differs from key i-1's: distinct cells of level l = counts[l] + 1.
+__global__ __launch_bounds__(256) void key_levels_kernel(const uint32_t *__restrict__ keys, int64_t n,
+                                                         unsigned long long *__restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = i >= 1 && i < n;
+  const uint32_t a = ok ? keys[i - 1] : 0u, b = ok ? keys[i] : 0u;
+  const uint32_t x = a ^ b;  // differing bits
+#pragma unroll
+  for (int l = 1; l <= 10; l++) {
+    const bool d = ok && (x >> (3 * (10 - l))) != 0u;
+    const uint64_t m = __ballot(d);
+    if (lsk::lane_id() == 0 && m) atomicAdd(&counts[l], (unsigned long long)__popcll(m));
+  }
+}
+
+// sum over sub-cells of (end - start)^2: the mean sub-cell population seen by a point is
+// this / n (uniform data: about the mean population + 1).
+__global__ __launch_bounds__(256) void grid_sq_kernel(const uint32_t *__restrict__ subs, int64_t nsub,
+                                                      unsigned long long *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long v = 0;
+  if (i < nsub) {
+    const uint32_t a = subs[2 * i], b = subs[2 * i + 1];
+    const unsigned long long d = b > a ? (unsigned long long)(b - a) : 0ull;
+    v = d * d;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lsk::lane_id() == 0 && v) atomicAdd(out, v);
+}
+
+}  // namespace
+
+extern "C" int lsk_hip_grid_build(const float *sorted_pts, int64_t n, const float *box, int32_t level,
+                                  uint32_t *cells, uint32_t *subs, void *stream) {
+  if (level < 1 || level > 9) {
+    lsk::set_last_error("grid_build: level must be in [1, 9] (sub-cells at level + 1 <= 10)");
+    return 1;
+  }
+  if (n >= ((int64_t)1 << 32)) {
+    lsk::set_last_error("grid_build: n must be < 2^32");
+    return 1;
+  }
+  const size_t ncell = (size_t)1 << (3 * level);
+  hipStream_t st = (hipStream_t)stream;
+  LSK_HIP(hipMemsetAsync(cells, 0, ncell * 8, st));
+  LSK_HIP(hipMemsetAsync(subs, 0, ncell * 64, st));
+  if (n <= 0) return 0;
+  grid_build_kernel<<<lsk_blocks(n, 256), 256, 0, st>>>(sorted_pts, n, box, (uint32_t)level + 1u, cells, subs);
+  LSK_CHECK_LAUNCH("grid_build");
+  return 0;
+}
+
+extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
+  if (n <= 1) return 0;
+  key_levels_kernel<<<lsk_blocks(n, 256), 256, 0, st>>>(keys, n, counts);
+  LSK_CHECK_LAUNCH("key_levels");
+  return 0;
+}
+
+extern "C" int lsk_hip_grid_sq(const uint32_t *subs, int64_t nsub, unsigned long long *out, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  LSK_HIP(hipMemsetAsync(out, 0, sizeof(unsigned long long), st));
+  if (nsub <= 0) return 0;
+  grid_sq_kernel<<<lsk_blocks(nsub, 256), 256, 0, st>>>(subs, nsub, out);
+  LSK_CHECK_LAUNCH("grid_sq");
+  return 0;
+}
+
+extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *stream) {
+  const lsk_knn_args &A = *args;
+  if (A.k < 1 || A.k > 65535) {
+    lsk::set_last_error("knn_grid: k must be in [1, 65535]");
+    return 1;
+  }
+  if (A.nq >= ((int64_t)1 << 32) || A.ntrees != 1 || A.groups || A.init_d2 ||
+      A.tree[0].n >= ((int64_t)1 << 32) || !grid || grid->level < 1 || grid->level > 9) {
+    lsk::set_last_error("knn_grid: one tree (< 2^32 points, the queries' own), no groups / init_d2, "
+                        "grid level in [1, 9]");
+    return 1;
+  }
+  const int64_t ngroups = (A.nq + 63) / 64;
+  if (ngroups <= 0) return 0;
+  knn_grid_kernel<<<lsk_blocks(ngroups, kWPB), kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+  LSK_CHECK_LAUNCH("knn_grid");
+  return 0;
+}

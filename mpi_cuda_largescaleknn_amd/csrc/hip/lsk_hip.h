@@ -138,6 +138,29 @@ int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream);
 int lsk_hip_knn_exact(const lsk_knn_args *args, const uint32_t *list, const uint32_t *count,
                       int64_t cap, void *stream);
 
+// ---- cell-grid candidate source (knn_grid.hip) -----------------------------------------
+// Two octree levels over the Hilbert-sorted points of one tree (cube = the sort keys' box):
+// cells of level `level` and their sub-cells (level + 1 <= 10), each a contiguous run of
+// the sorted array stored as a (start, end) uint32 pair at its Morton index (empty: 0, 0).
+typedef struct lsk_grid_view {
+  const uint32_t *cells;  // [8^level][2]
+  const uint32_t *subs;   // [8^(level+1)][2]
+  const float *box;       // [8] device: the box of the sort keys (lo.xyz, hi.xyz, scale, extent)
+  const float *inf4;      // [4] device: +inf (candidate padding)
+  int32_t level;
+  int32_t pad;
+} lsk_grid_view;
+int lsk_hip_grid_build(const float *sorted_pts, int64_t n, const float *box, int32_t level, uint32_t *cells,
+                       uint32_t *subs, void *stream);
+// counts[l] (l = 1..10, 11 slots, zeroed here) = number of adjacent sorted keys whose level-l
+// prefixes differ (distinct level-l cells = counts[l] + 1).
+int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream);
+// out[0] = sum over sub-cells of population^2 (zeroed here).
+int lsk_hip_grid_sq(const uint32_t *subs, int64_t nsub, unsigned long long *out, void *stream);
+// Near-uniform fast path of lsk_hip_knn_rows (same contract, same failure list): one tree
+// whose points are the queries, no groups / init_d2; candidates from the grid.
+int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *stream);
+
 // ---- halo exchange -------------------------------------------------------------------
 // Published tree: the top `levels` levels of a tree (node slots 1 .. 2^levels-1... up to
 // 2^(levels+1)), each node 8 floats (lo.xyz, r2, hi.xyz, pad).

@@ -13,6 +13,7 @@ halo tree in the distributed pipelines).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -49,6 +50,29 @@ class KnnConfig:
         return cut2_of(self.max_radius)
 
 
+# Cell-grid candidate source of the local k-NN pass (knn_grid.hip): "auto" = built for
+# GPU indexes whose sub-cell populations look near-uniform (GRID_CROWD), "on" = always,
+# "off" = never (the bucket-tree kernel knn_rows serves every query).
+GRID = os.environ.get("LSKNN_GRID", "auto")
+GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "4"))  # target mean points per sub-cell
+# auto: a point's sub-cell holds on average at most this many times the mean (+1)
+GRID_CROWD = float(os.environ.get("LSKNN_GRID_CROWD", "3"))
+
+
+@dataclass
+class GridIndex:
+    cells: torch.Tensor      # int32 [8^level, 2] (start, end) of each level-`level` cell
+    subs: torch.Tensor       # int32 [8^(level+1), 2] of each sub-cell
+    level: int
+    box: torch.Tensor        # the cube of the sort keys (device)
+    inf4: torch.Tensor | None = None  # 4 x +inf on the device (candidate padding)
+
+    def view(self) -> tuple:
+        if self.inf4 is None:
+            self.inf4 = torch.full((4,), math.inf, dtype=torch.float32, device=self.cells.device)
+        return (self.cells, self.subs, self.level, self.box, self.inf4)
+
+
 @dataclass
 class LocalIndex:
     n: int
@@ -58,6 +82,7 @@ class LocalIndex:
     qnodes: torch.Tensor     # [2^depth * 4, 8] boxes of each bucket's four 16-point quarters
     depth: int
     box: torch.Tensor        # [8] cube used for the Morton keys
+    grid: GridIndex | None = None
 
     @property
     def device(self) -> torch.device:
@@ -89,10 +114,11 @@ class KnnStats:
 
 
 def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
-                keys: tuple | None = None) -> LocalIndex:
+                keys: tuple | None = None, grid: bool = False) -> LocalIndex:
     """Sort points along the space-filling curve of `box` (default: their own bounds) and
     build the bucket tree. `keys` = (keys, iota) computed already (the streamed upload
-    keys each chunk as it lands)."""
+    keys each chunk as it lands). `grid`: also index the sorted points by the cell grid of
+    the fast local k-NN pass (build_grid; GPU, outside graph captures)."""
     points = points.contiguous()
     n = points.shape[0]
     if box is None:
@@ -102,7 +128,39 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     perm = refine_heavy_cells(points, skeys, perm)
     pts = K.gather3(points, perm, pad=K.PAD_POINTS)
     nodes, qnodes, depth = K.build_tree(pts, n)
-    return LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
+    index = LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
+    if grid:
+        index.grid = build_grid(index, skeys)
+    return index
+
+
+def grid_level(distinct: list[int], n: int, ms: float = GRID_MS) -> int:
+    """Sub-cell level of the grid: the finest level whose occupied sub-cells hold at least
+    `ms` points on average (uniform 1B points in a cube: 9, 1e8: 8, 1e7: 7), in [2, 10]."""
+    ls = 2
+    for lvl in range(2, 11):
+        if distinct[lvl] > 0 and n / distinct[lvl] >= ms:
+            ls = lvl
+    return ls
+
+
+def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
+    """Cell grid over index's sorted points (knn_grid.hip), or None when it does not apply
+    (CPU, graph capture, GRID=off, or crowded sub-cells under GRID=auto: clustered or
+    multi-scale data keeps the bucket-tree walk of knn_rows, which adapts to density).
+    Two host reads (the level census and the crowding sum)."""
+    n = index.n
+    if GRID == "off" or n == 0 or not K.is_gpu(index.pts) or torch.cuda.is_current_stream_capturing():
+        return None
+    distinct = K.key_levels(skeys[:n])
+    ls = grid_level(distinct, n)
+    cells, subs = K.grid_build(index.pts, n, index.box, ls - 1)
+    if GRID == "auto":
+        seen = K.grid_sq(subs) / n          # mean population of a point's own sub-cell
+        mean = n / max(1, distinct[ls])
+        if seen > GRID_CROWD * (mean + 1.0):
+            return None
+    return GridIndex(cells, subs, ls - 1, index.box)
 
 
 HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key
@@ -292,8 +350,12 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
     kw = dict(groups=groups, ngroups=ngroups, seed=SEED_BUCKETS, init_d2=init_d2,
               out_perm=index.perm if final_out is not None else None, out_final=final_out)
+    impl = KNN_IMPL
+    use_grid = (impl == "rows" and index.grid is not None and len(trees) == 1 and groups is None
+                and init_d2 is None and cfg.k <= K.ROWS_MAX_K)
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
-                   impl=KNN_IMPL, debug_fail_mod=DEBUG_FAIL_MOD, **kw)
+                   impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
+                   grid=index.grid.view() if use_grid else None, **kw)
     def check():
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun
         # the whole query on the exact kernel
@@ -344,7 +406,7 @@ def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,
     """Distance from every point to its k-th nearest neighbour among `points`
     (itself counted), in input order — the single-rank reference output."""
     cfg = KnnConfig(k=k, max_radius=max_radius)
-    index = build_index(points)
+    index = build_index(points, grid=True)
     hint2 = radius_hint(index.box, index.n, k)
     out = torch.empty(index.n, dtype=torch.float32, device=points.device)
     return query(index, cfg, hint2, stats=stats, final_out=out)

@@ -17,7 +17,7 @@ import os
 import torch
 
 from .. import _native
-from .._native import KnnArgs, TreeView, check
+from .._native import GridView, KnnArgs, TreeView, check
 
 BUCKET = 64
 PAD_POINTS = 64  # readable padding required after point arrays read by the knn kernel
@@ -256,7 +256,8 @@ class FailWord:
         self.cap = cap
 
     def value(self) -> int:
-        return 0 if self.count is None else int(self.count.item())
+        # the kernels count in uint32 (a count >= 2^31 must not read as negative)
+        return 0 if self.count is None else int(self.count.item()) & 0xFFFFFFFF
 
     def overflowed(self) -> bool:
         return self.value() > self.cap
@@ -268,7 +269,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
-            debug_fail_mod: int = 0) -> FailWord:
+            debug_fail_mod: int = 0, grid=None) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -282,6 +283,9 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     out_perm / out_final (optional, fused scatter): the kernels also write
     out_final[out_perm[q]] = final distance; out_d2 may then be None.
     debug_fail_mod (tests): the rows kernel also fails every query q with q % mod == 0.
+    grid (impl "grid"): (cells, subs, level, box) of knn_engine.GridIndex — the cell-grid
+    candidate source of knn_grid.hip for one tree whose points are the queries (same
+    failure list and backstop as "rows").
     Returns the launch's FailWord.
     """
     if (out_perm is None) != (out_final is None):
@@ -289,8 +293,10 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     if out_perm is not None and (out_perm.shape[0] < nq or out_perm.dtype != torch.int32
                                  or not out_perm.is_contiguous() or out_final.dtype != torch.float32):
         raise ValueError("knn_gpu: out_perm must be int32 [>= nq], out_final float32")
-    if impl not in ("rows", "exact"):
-        raise ValueError(f"knn_gpu: impl must be rows or exact, not {impl!r}")
+    if impl not in ("rows", "exact", "grid"):
+        raise ValueError(f"knn_gpu: impl must be rows, exact or grid, not {impl!r}")
+    if impl == "grid" and (grid is None or len(trees) != 1 or groups is not None or init_d2 is not None):
+        raise ValueError("knn_gpu: impl grid needs a grid, one tree, no groups and no init_d2")
     a = KnnArgs()
     a.qpts = _ptr(qpts)
     a.nq = nq
@@ -328,10 +334,46 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_list = _ptr(flist)
     a.fail_count = _ptr(count)
     a.fail_cap = cap
-    check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
+    if impl == "grid":
+        cells, subs, level, gbox, inf4 = grid
+        gv = GridView(_ptr(cells), _ptr(subs), _ptr(gbox), _ptr(inf4), int(level), 0)
+        check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
+    else:
+        check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
     # exact backstop over the failure list (device-side count: empty list = short no-op)
     check(lib.lsk_hip_knn_exact(C.byref(a), _ptr(flist), _ptr(count), cap, st), "knn_exact")
     return FailWord(count, cap)
+
+
+# --------------------------------------------------------------------------- cell grid
+def key_levels(skeys: torch.Tensor) -> list[int]:
+    """Distinct cells of each octree level 0..10 among sorted 30-bit curve keys (one
+    device pass + one 88-byte read): [1, d1, ..., d10]."""
+    n = skeys.shape[0]
+    if n == 0:
+        return [0] * 11
+    cnt = torch.empty(11, dtype=torch.int64, device=skeys.device)
+    check(_native.hip().lsk_hip_key_levels(_ptr(skeys), n, _ptr(cnt), _stream(skeys)), "key_levels")
+    c = cnt.cpu().tolist()
+    return [1] + [int(c[l]) + 1 for l in range(1, 11)]
+
+
+def grid_build(sorted_pts: torch.Tensor, n: int, box: torch.Tensor, level: int):
+    """(start, end) runs of the level-`level` cells and their level+1 sub-cells along the
+    sorted points (knn_grid.hip) -> (cells [8^level, 2], subs [8^(level+1), 2]) int32."""
+    dev = sorted_pts.device
+    cells = torch.empty((1 << (3 * level), 2), dtype=torch.int32, device=dev)
+    subs = torch.empty((1 << (3 * level + 3), 2), dtype=torch.int32, device=dev)
+    check(_native.hip().lsk_hip_grid_build(_ptr(sorted_pts), n, _ptr(box), level, _ptr(cells), _ptr(subs),
+                                           _stream(sorted_pts)), "grid_build")
+    return cells, subs
+
+
+def grid_sq(subs: torch.Tensor) -> int:
+    """Sum over sub-cells of population^2 (host read)."""
+    out = torch.empty(1, dtype=torch.int64, device=subs.device)
+    check(_native.hip().lsk_hip_grid_sq(_ptr(subs), subs.shape[0], _ptr(out), _stream(subs)), "grid_sq")
+    return int(out.item())
 
 
 def kth_cpu(points: torch.Tensor, queries: torch.Tensor, k: int, cut2: float, method: str = "kdtree") -> torch.Tensor:

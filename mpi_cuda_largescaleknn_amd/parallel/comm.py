@@ -35,6 +35,12 @@ class Comm:
     # True: run every collective through the backend even on a 1-rank group, and the
     # pipelines take their multi-rank path (tests: exercises each RCCL call site on one GPU)
     force: bool = False
+    # collective / grouped point-to-point launches handed to the backend so far (bench.py
+    # reports them per step: the control plane's cost on a real multi-GPU run)
+    ncoll: int = 0
+
+    def collectives(self) -> int:
+        return self.ncoll
 
     @property
     def distributed(self) -> bool:
@@ -140,6 +146,7 @@ class TorchComm(Comm):
 
     def allreduce_(self, t, op="sum"):
         if self.distributed:
+            self.ncoll += 1
             if self.staged and t.device.type != "cpu":
                 h = t.cpu()
                 dist.all_reduce(h, op=_OPS[op], group=self.group)
@@ -151,11 +158,13 @@ class TorchComm(Comm):
     def allgather(self, t):
         t = t.contiguous()
         if self.staged and t.device.type != "cpu" and self.distributed:
+            self.ncoll += 1
             return self._gather_gloo(t.cpu()).to(t.device)
         if not self.distributed:
             out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
             out[0].copy_(t)
             return out
+        self.ncoll += 1
         if self.backend == "gloo":
             return self._gather_gloo(t)
         out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
@@ -178,22 +187,14 @@ class TorchComm(Comm):
         staged = self.staged and dev.type != "cpu"
         src = send.cpu() if staged else send.contiguous()
         recv = torch.empty((sum(recv_counts), *row_shape), dtype=send.dtype, device=src.device)
-        row_bytes = src.element_size() * math.prod(row_shape)
-        # one collective form on every rank: all_to_all_single when no message of the
-        # exchange exceeds the cap, else the piece rounds. A rank only sees its own rows
-        # and columns of the count matrix, so the largest message is agreed first (a rank
-        # choosing all_to_all_single while a peer posts point-to-point pieces would hang)
-        big = torch.tensor([max(send_counts + recv_counts + [0]) * row_bytes], dtype=torch.int64,
-                           device=self._device if not self.staged else torch.device("cpu"))
-        dist.all_reduce(big, op=dist.ReduceOp.MAX, group=self.group)
-        if int(big.item()) <= self.max_msg_bytes:
-            dist.all_to_all_single(recv, src, output_split_sizes=recv_counts,
-                                   input_split_sizes=send_counts, group=self.group)
-        else:
-            so, ro = _offsets(send_counts), _offsets(recv_counts)
-            sends = [(j, src[so[j]:so[j + 1]]) for j in range(self.size)]
-            recvs = [(j, recv[ro[j]:ro[j + 1]]) for j in range(self.size)]
-            self._p2p_rounds(sends, recvs)
+        # grouped send/recv (the all-to-all-v RCCL itself runs: ncclSend/ncclRecv per peer in
+        # one group), every message cut into pieces of at most max_msg_bytes. Both ends of a
+        # pair know that message's size, so the pieces match pair by pair with no agreement
+        # on a global collective form first (no extra all-reduce or host sync per exchange)
+        so, ro = _offsets(send_counts), _offsets(recv_counts)
+        sends = [(j, src[so[j]:so[j + 1]]) for j in range(self.size)]
+        recvs = [(j, recv[ro[j]:ro[j + 1]]) for j in range(self.size)]
+        self._p2p_rounds(sends, recvs)
         return (recv.to(dev) if staged else recv), recv_counts
 
     def _p2p_rounds(self, sends, recvs):
@@ -226,6 +227,7 @@ class TorchComm(Comm):
             ops = [dist.P2POp(dist.isend, p[r], j, group=self.group) for j, p in ps if r < len(p)]
             ops += [dist.P2POp(dist.irecv, p[r], j, group=self.group) for j, p in pr if r < len(p)]
             if ops:
+                self.ncoll += 1
                 for req in dist.batch_isend_irecv(ops):
                     req.wait()
 
@@ -242,6 +244,7 @@ class TorchComm(Comm):
 
     def barrier(self):
         if self.distributed:
+            self.ncoll += 1
             if self.backend == "nccl":
                 # device barrier via a 1-element all-reduce keeps RCCL the only channel
                 t = torch.zeros(1, device=self._device)
@@ -290,6 +293,7 @@ class LoopbackComm(Comm):
             torch.cuda.current_stream(self._device).synchronize()
 
     def _share(self, obj):
+        self.ncoll += 1
         self._sync_device()
         self.hub.slots[self.rank] = obj
         self.hub.barrier.wait()
@@ -334,6 +338,7 @@ class LoopbackComm(Comm):
         return recv, counts
 
     def barrier(self):
+        self.ncoll += 1
         self._sync_device()
         self.hub.barrier.wait()
 

@@ -93,6 +93,9 @@ class MonitoredComm(Comm):
     def device(self):
         return self.inner.device
 
+    def collectives(self) -> int:
+        return self.inner.collectives()
+
     def _enter(self, op: str) -> None:
         HEARTBEAT.beat(op)
         n = self.calls.get(op, 0)

@@ -181,14 +181,30 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
     return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
 
 
+def launcher_env() -> bool:
+    """True when a launcher (torchrun, spawn_local, mpirun) has set this process's rank."""
+    return any(os.environ.get(v) not in (None, "") for v in
+               ("RANK", "WORLD_SIZE", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "PMIX_RANK"))
+
+
 def spawn_local(nproc: int, module: str, argv: list[str]) -> int:
     """--bootstrap spawn: start `nproc` local ranks of `python -m module argv...` (each
     with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* set, bootstrap env) and wait for them.
     Called before anything touches the GPU. A failing rank's peers abort through the
     watchdog; the launcher returns the first non-zero exit code."""
+    import sys
+
+    return spawn_ranks(nproc, [sys.executable, "-m", module, *argv, "--bootstrap", "env"])
+
+
+def spawn_ranks(nproc: int, cmd: list[str]) -> int:
+    """Run `cmd` as `nproc` local ranks (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
+    MASTER_PORT on a free loopback port), the torchrun contract, and wait for all of them.
+    Must be called before this process touches the GPU (the children open it). Returns
+    the first non-zero exit code; once a rank fails, the others get 60 s to end through
+    the abort broadcast (parallel/faults.py) before they are terminated."""
     import socket
     import subprocess
-    import sys
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -198,11 +214,26 @@ def spawn_local(nproc: int, module: str, argv: list[str]) -> int:
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_RANK=str(r),
                    LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-m", module, *argv, "--bootstrap", "env"], env=env))
+        procs.append(subprocess.Popen(cmd, env=env))
     rc = 0
-    for p in procs:
-        code = p.wait()
-        rc = rc or code
+    live = list(procs)
+    deadline = None
+    import time
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is not None:
+                live.remove(p)
+                if code and not rc:
+                    rc = code
+                    deadline = time.monotonic() + 60.0
+        if live and deadline is not None and time.monotonic() > deadline:
+            for p in live:
+                p.terminate()
+            for p in live:
+                p.wait()
+            break
+        time.sleep(0.05)
     return rc
 
 

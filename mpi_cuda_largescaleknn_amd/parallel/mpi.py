@@ -100,6 +100,7 @@ class MpiComm(Comm):
         if t.dtype not in _DTYPES:
             raise TypeError(f"MpiComm.allreduce_: unsupported dtype {t.dtype}")
         h = self._host(t)
+        self.ncoll += 1
         _check(_native.mpi().lsk_mpi_allreduce(h.data_ptr(), h.numel(), _DTYPES[h.dtype], _OPS[op]),
                "MPI_Allreduce")
         if h.data_ptr() != t.data_ptr():
@@ -112,6 +113,7 @@ class MpiComm(Comm):
         if not self.distributed:
             out[0].copy_(h)
         else:
+            self.ncoll += 1
             _check(_native.mpi().lsk_mpi_allgather(h.data_ptr(), out.data_ptr(), h.numel() * h.element_size(),
                                                    self.max_msg_bytes), "MPI_Allgather")
         return out if t.device.type == "cpu" else out.to(t.device)
@@ -129,6 +131,7 @@ class MpiComm(Comm):
         arr = lambda v: (C.c_int64 * len(v))(*v)  # noqa: E731
         so = [o * rb for o in _offsets(send_counts)[:-1]]
         ro = [o * rb for o in _offsets(recv_counts)[:-1]]
+        self.ncoll += 1
         _check(_native.mpi().lsk_mpi_alltoallv(
             self.size, src.data_ptr(), arr(so), arr([c * rb for c in send_counts]), recv.data_ptr(), arr(ro),
             arr([c * rb for c in recv_counts]), self.max_msg_bytes, int(self.force)), "MPI all-to-all-v")
@@ -154,6 +157,7 @@ class MpiComm(Comm):
             ints = lambda v: (C.c_int * max(1, len(v)))(*v)  # noqa: E731
             ptrs = lambda v: (C.c_void_p * max(1, len(v)))(*v)  # noqa: E731
             i64s = lambda v: (C.c_int64 * max(1, len(v)))(*v)  # noqa: E731
+            self.ncoll += 1
             _check(_native.mpi().lsk_mpi_sendrecv(
                 len(sp), ints([d for d, _ in sp]), ptrs([t.data_ptr() for _, t in sp]),
                 i64s([t.numel() * t.element_size() for _, t in sp]), len(rp), ints([s for s, _ in rp]),
@@ -165,4 +169,5 @@ class MpiComm(Comm):
         if self.distributed:
             if self._device.type == "cuda":
                 torch.cuda.synchronize(self._device)
+            self.ncoll += 1
             _check(_native.mpi().lsk_mpi_barrier(), "MPI_Barrier")

@@ -683,7 +683,7 @@ def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int
     hint2 = E.radius_hint(box, n_total, cfg.k)
     info.timer.mark("bounds")
     info.counts["owned_points"] = n_local
-    index = E.build_index(points, box, keys=keys)
+    index = E.build_index(points, box, keys=keys, grid=True)
     info.timer.mark("build")
     return index, hint2
 
@@ -729,7 +729,7 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     R = redistribute_stream(points, comm, info)
     box, owned = R.box, R.owned
     hint2 = E.radius_hint(box, n_total, cfg.k)
-    index = E.build_index(owned, box)
+    index = E.build_index(owned, box, grid=True)
     info.timer.mark("build")
     # final distances in received-row order straight from the kernels (fused scatter);
     # the sorted d2 feeds the halo radii and the re-query bounds
@@ -787,7 +787,7 @@ def compute_set(P: Redistributed, comm: Comm, cfg: E.KnnConfig, info: RunInfo | 
     return is ordered after it (one communicator: no concurrent collectives)."""
     info = info or RunInfo(PhaseTimer(False, comm.device))
     dev = comm.device
-    index = E.build_index(P.owned, P.box)
+    index = E.build_index(P.owned, P.box, grid=True)
     info.timer.mark("build")
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     used: list = []
@@ -848,7 +848,7 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     gbox = global_box(points, comm) if comm.distributed else box
     hint2 = E.radius_hint(gbox, n_total, cfg.k)
     info.timer.mark("bounds")
-    index = E.build_index(points, box)
+    index = E.build_index(points, box, grid=True)
     info.counts["owned_points"] = n_local
     info.timer.mark("build")
     if not comm.distributed:  # fused scatter: final distances straight from the k-NN kernel

@@ -127,6 +127,7 @@ class RcclComm(Comm):
         if not self.distributed:
             return t
         d = self._dev(t).contiguous()
+        self.ncoll += 1
         _check(_native.comm().lsk_comm_allreduce(self._h, d.data_ptr(), d.numel(), _DTYPES[d.dtype], _OPS[op],
                                                  _stream(self._device)), "allreduce")
         if d.data_ptr() != t.data_ptr():
@@ -139,6 +140,7 @@ class RcclComm(Comm):
         if not self.distributed:
             out[0].copy_(d)
         else:
+            self.ncoll += 1
             _check(_native.comm().lsk_comm_allgather(self._h, d.data_ptr(), out.data_ptr(),
                                                      d.numel() * d.element_size(), _stream(self._device)),
                    "allgather")
@@ -157,6 +159,7 @@ class RcclComm(Comm):
         so = [o * rb for o in _offsets(send_counts)[:-1]]
         ro = [o * rb for o in _offsets(recv_counts)[:-1]]
         arr = lambda v: (C.c_int64 * len(v))(*v)  # noqa: E731
+        self.ncoll += 1
         _check(_native.comm().lsk_comm_alltoallv(
             self._h, self.size, self.rank, src.data_ptr(), arr(so), arr([c * rb for c in send_counts]),
             recv.data_ptr(), arr(ro), arr([c * rb for c in recv_counts]), self.max_msg_bytes, int(self.force),
@@ -183,6 +186,7 @@ class RcclComm(Comm):
             ints = lambda v: (C.c_int * max(1, len(v)))(*v)  # noqa: E731
             ptrs = lambda v: (C.c_void_p * max(1, len(v)))(*v)  # noqa: E731
             i64s = lambda v: (C.c_int64 * max(1, len(v)))(*v)  # noqa: E731
+            self.ncoll += 1
             _check(_native.comm().lsk_comm_sendrecv(
                 self._h, len(sp), ints([d for d, _ in sp]), ptrs([t.data_ptr() for _, t in sp]),
                 i64s([t.numel() * t.element_size() for _, t in sp]), len(rp), ints([s for s, _ in rp]),

@@ -172,3 +172,46 @@ def test_bench_two_gpu_ranks_pipelined_gloo():
     assert rec["config"]["all_finite"] is True
     assert rec["config"]["sampled_exact"] == "512/512"
     assert sum(rec["detail"]["owned_points_per_rank"]) == 400000
+
+
+def test_bench_self_launches_gpus_ranks_on_cpu():
+    """`bench.py --gpus 4` with no launcher environment starts 4 local ranks itself (the
+    reference's `mpirun -n P`, README.md:31,39) and reports them; no torchrun involved."""
+    env = _env()
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--device", "cpu", "--points", "3e4",
+                          "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 4 and rec["config"]["ranks"] == 4
+    assert rec["config"]["comm"] == "gloo"
+    assert rec["config"]["sampled_exact"] == "256/256"
+    assert rec["config"]["collectives_per_step"] > 0
+    assert len(rec["detail"]["owned_points_per_rank"]) == 4
+
+
+def test_bench_launcher_world_size_must_match_gpus():
+    env = _env()
+    env.update(RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--device", "cpu", "--points", "3e4"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0
+    assert "started 2 ranks but --gpus is 4" in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_two_ranks_one_gpu_gloo():
+    """Two self-launched ranks sharing the one GPU (gloo: RCCL refuses two ranks on one
+    device): the full multi-rank GPU pipeline, outputs sampled exact."""
+    env = _env()
+    env["LSKNN_DIST_BACKEND"] = "gloo"
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--points", "4e5", "--steps", "2",
+                          "--warmup", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["ranks"] == 2
+    assert rec["config"]["sampled_exact"] == "256/256"

@@ -1,0 +1,110 @@
+"""Cell-grid k-NN pass (knn_grid.hip): grid tables against a torch reference, and the
+k-th distances bit for bit against the C++ CPU oracle on every data distribution."""
+import math
+
+import pytest
+import torch
+
+from datasets import GENERATORS, uniform
+from mpi_cuda_largescaleknn_amd.models import knn_engine as E
+from mpi_cuda_largescaleknn_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def oracle(points, k, max_radius=math.inf):
+    return K.finalize_distances(K.kth_cpu(points, points, k, E.cut2_of(max_radius)))
+
+
+def grid_knn(p, k, max_radius=math.inf, mode="on"):
+    old = E.GRID
+    E.GRID = mode
+    try:
+        cfg = E.KnnConfig(k=k, max_radius=max_radius)
+        idx = E.build_index(p.to(DEV), grid=True)
+        st = E.KnnStats()
+        out = torch.empty(idx.n, dtype=torch.float32, device=DEV)
+        E.query(idx, cfg, E.radius_hint(idx.box, idx.n, k), stats=st, final_out=out)
+        return out.cpu(), idx, st
+    finally:
+        E.GRID = old
+
+
+@pytest.mark.parametrize("n", [1, 100, 5000, 200_003])
+def test_grid_tables_match_torch(n):
+    p = uniform(n, seed=n).to(DEV)
+    idx = E.build_index(p)
+    for level in (1, 3, 5):
+        cells, subs = K.grid_build(idx.pts, n, idx.box, level)
+        box = idx.box.cpu()
+        q = ((idx.pts[:n].cpu() - box[0:3]) * box[6]).clamp(0, 1023).to(torch.int64)
+        for lv, tab in ((level, cells), (level + 1, subs)):
+            c = q >> (10 - lv)
+            m = torch.zeros(n, dtype=torch.int64)
+            for b in range(lv):  # Morton index: x bit 2, y bit 1, z bit 0 of each triple
+                for a, sh in ((0, 2), (1, 1), (2, 0)):
+                    m |= ((c[:, a] >> b) & 1) << (3 * b + sh)
+            assert bool((m[1:] != m[:-1]).sum() + 1 == torch.unique(m).numel())  # runs contiguous
+            ref = torch.zeros((1 << (3 * lv), 2), dtype=torch.int64)
+            uniq, first = torch.unique_consecutive(m, return_counts=True)
+            starts = torch.cumsum(first, 0) - first
+            ref[uniq, 0] = starts
+            ref[uniq, 1] = starts + first
+            assert torch.equal(tab.cpu().to(torch.int64), ref)
+
+
+@pytest.mark.parametrize("dist", list(GENERATORS))
+@pytest.mark.parametrize("k", [1, 8, 16, 100])
+def test_grid_knn_matches_oracle(dist, k):
+    p = GENERATORS[dist](30000, seed=k + 7)
+    ref = oracle(p, k)
+    got, idx, st = grid_knn(p, k)
+    assert idx.grid is not None
+    bad = (got != ref) & ~(torch.isnan(got) & torch.isnan(ref))
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} mismatches; stats={st.counters}"
+    assert torch.isfinite(got).all()
+
+
+@pytest.mark.parametrize("k", [1, 5, 64, 100])
+def test_grid_knn_cutoff(k):
+    p = uniform(20000, seed=3)
+    r = 0.02
+    ref = oracle(p, k, r)
+    got, _, _ = grid_knn(p, k, r)
+    assert torch.equal(got, ref)
+
+
+def test_grid_knn_k_larger_than_n_and_tiny_sets():
+    for n in (1, 2, 63, 64, 65, 130):
+        p = uniform(n, seed=n)
+        for k in (1, 3, 64, 200):
+            got, _, _ = grid_knn(p, k)
+            assert torch.equal(got, oracle(p, k)), (n, k)
+
+
+def test_grid_uniform_large_equals_rows_bitwise():
+    p = uniform(2_000_000, seed=11).to(DEV)
+    for k in (16, 100):
+        got, idx, st = grid_knn(p, k)
+        old = E.KNN_IMPL
+        idx.grid = None
+        out = torch.empty(idx.n, dtype=torch.float32, device=DEV)
+        E.query(idx, E.KnnConfig(k=k), E.radius_hint(idx.box, idx.n, k), final_out=out)
+        assert E.KNN_IMPL == old
+        assert torch.equal(got, out.cpu())
+        assert st.counters.get("failed_lanes", 0) == 0
+
+
+def test_grid_auto_skips_crowded_data():
+    # mixed-scale data: a dense core far below one sub-cell of the global cube
+    p = GENERATORS["mixed_scale"](200_000, seed=2).to(DEV)
+    old = E.GRID
+    E.GRID = "auto"
+    try:
+        idx = E.build_index(p, grid=True)
+        assert idx.grid is None
+        idx = E.build_index(uniform(200_000, seed=2).to(DEV), grid=True)
+        assert idx.grid is not None
+    finally:
+        E.GRID = old
