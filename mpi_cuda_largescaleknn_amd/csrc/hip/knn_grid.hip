@@ -45,15 +45,30 @@ constexpr int kThreads = kWPB * lsk::kWave;
 constexpr int kBins = 40;                 // 16-bit bins, two per LDS dword (as knn_rows)
 constexpr int kPool = kBins / 2 * 64;     // dwords per wave: histogram, or collect pool
 #ifndef LSK_GRID_TOPBINS
-#define LSK_GRID_TOPBINS 12
+#define LSK_GRID_TOPBINS 10
 #endif
-constexpr int kTopBins = LSK_GRID_TOPBINS;  // first range tops out 1.5 octaves above the estimate
+// first range tops out 1.25 octaves of d² above the estimate (1e8 uniform, k=100, nearest-
+// first cells: 8 bins 0.1207 s with 82K overflow lanes, 10 bins 0.1181 s / 6.8K, 12 bins
+// 0.1197 s / 623)
+constexpr int kTopBins = LSK_GRID_TOPBINS;
 constexpr uint32_t kLogBins = 5;          // floor(log2(kBins))
 constexpr uint32_t kShift0 = 20;          // 1/8 octave of d² per bin
 constexpr uint32_t kMaxPasses = 24;
 constexpr uint32_t kUnknown = 0xffffffffu;
 constexpr uint32_t kNaNBits = 0x7fc00000u;
 constexpr float kEstCalib = 0.8f;
+
+// LSK_GRID_PROFILE builds (tuning only): shader-clock cycles per wave in candidate
+// processing / cell enumeration of each pass kind, and the whole wave, into
+// stats[16..19] and [23] (knn_engine.KnnStats prof_* names), evals per pass kind in
+// stats[12] (HIST) and [13] (COLLECT).
+#ifdef LSK_GRID_PROFILE
+#define LSK_GT(v) const uint64_t v = __builtin_readcyclecounter()
+#define LSK_GADD(acc, t0) (acc) += __builtin_readcyclecounter() - (t0)
+#else
+#define LSK_GT(v)
+#define LSK_GADD(acc, t0)
+#endif
 
 enum : uint32_t { ST_HIST = 0, ST_READY = 1, ST_DONE = 2 };
 enum { MODE_HIST = 0, MODE_COLLECT = 1 };
@@ -149,6 +164,18 @@ __device__ __forceinline__ float wave_max_nonneg(float v) {
   return __uint_as_float(max(max(a, b), max(c, d)));
 }
 
+__device__ __forceinline__ float wave_min_nonneg(float v) {
+  v = fminf(v, dpp_f<0xB1>(v));
+  v = fminf(v, dpp_f<0x4E>(v));
+  v = fminf(v, dpp_f<0x124>(v));
+  v = fminf(v, dpp_f<0x128>(v));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 0);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 32);
+  const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 48);
+  return __uint_as_float(min(min(a, b), min(c, d)));
+}
+
 __device__ __forceinline__ float bcast64(float v, uint32_t j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
 }
@@ -212,6 +239,10 @@ struct GridCtx {
   int lane;
   uint32_t k;
   uint32_t evals, cells_n, segs;
+#ifdef LSK_GRID_PROFILE
+  uint64_t prof[8];
+  uint32_t ev_mode[2];
+#endif
 };
 
 // Cell coordinate at level l (monotone in v: a point with coordinate v' <= v never lies in
@@ -268,6 +299,20 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
     if (!__ballot(um < s.hi_b)) return;
     const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
     const uint32_t u[4] = {u0, u1, u2, u3};
+#ifdef LSK_GRID_BRANCHLESS
+    // every slot adds (0 when out of range): no exec-mask round trip per candidate
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const uint32_t v = u[t];
+      const bool in = v < hb;
+      const uint32_t w = __builtin_elementwise_sub_sat(min(v, hb - 1u), lb);
+      const uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
+      const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
+      atomicAdd(&pool[dw * lsk::kWave + lane], in ? __umul24(half, 0xffffu) + 1u : 0u);
+      s.c_hi += in ? 1u : 0u;
+    }
+    return;
+#endif
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const uint32_t v = u[t];
@@ -355,6 +400,9 @@ __device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0
   }
   G.evals += (i1 - i0 + 3u) & ~3u;
   G.segs++;
+#ifdef LSK_GRID_PROFILE
+  G.ev_mode[MODE] += (i1 - i0 + 3u) & ~3u;
+#endif
 }
 
 template <int MODE>
@@ -393,6 +441,7 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
   const uint32_t nonempty = (uint32_t)__ballot(sub);
   const uint32_t need = (uint32_t)__ballot(sub && g2 <= r2);
   if (need == 0u) return;
+  LSK_GT(tp0);
   if (need == nonempty) {
     process_segment<MODE>(s, G, cs, ce);
   } else {
@@ -405,6 +454,7 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
     }
   }
   shrink_all<MODE>(s, G);
+  LSK_GADD(G.prof[MODE], tp0);
 }
 
 // One pass over every cell within the cull radius of the wave's query box (cells that
@@ -418,7 +468,18 @@ constexpr uint32_t kMaxCells = 4096;
 constexpr uint32_t kScanAll = 1u << 16;
 
 template <int MODE>
-__device__ bool grid_pass(Lane &s, GridCtx &G, uint32_t n) {
+__device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n);
+
+template <int MODE>
+__device__ __forceinline__ bool grid_pass(Lane &s, GridCtx &G, uint32_t n) {
+  LSK_GT(tw0);
+  const bool ok = grid_pass_impl<MODE>(s, G, n);
+  LSK_GADD(G.prof[2 + MODE], tw0);
+  return ok;
+}
+
+template <int MODE>
+__device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
   float r2 = cull_r2<MODE>(s, G);
   if (fbits(r2) == 0u) return true;
   const uint32_t sh = 10u - G.lc;
@@ -432,12 +493,55 @@ __device__ bool grid_pass(Lane &s, GridCtx &G, uint32_t n) {
     shrink_all<MODE>(s, G);
     return true;
   }
+  CellLoad pend{0u, 0u, 0u, 0u, 0u};
+  bool have = false;
+  const uint32_t nx = x1 - x0 + 1u, ny = y1 - y0 + 1u, nz = z1 - z0 + 1u;
+  if (nx <= 16u && ny <= 16u && nx * ny * nz <= 256u) {
+    // Nearest first: lane l holds range cells l, l+64, l+128, l+192 with their gap to the
+    // wave box; each round takes the smallest gap still within the (shrinking) radius, so
+    // the bounds tighten before the farther cells are reached.
+    const uint32_t tot = nx * ny * nz;
+    const uint32_t inx = (65536u + nx - 1u) / nx, iny = (65536u + ny - 1u) / ny;  // exact for c < 256
+    auto gap_of = [&](uint32_t c) {
+      const uint32_t q = (c * inx) >> 16, r = (q * iny) >> 16;
+      return c < tot ? cell_gap2(G, x0 + c - q * nx, y0 + q - r * ny, z0 + r, sh) : __builtin_inff();
+    };
+    const uint32_t l = (uint32_t)G.lane;
+    float g0 = gap_of(l), g1 = gap_of(l + 64u), g2 = tot > 128u ? gap_of(l + 128u) : __builtin_inff();
+    float g3 = tot > 192u ? gap_of(l + 192u) : __builtin_inff();
+    for (;;) {
+      const float m = wave_min_nonneg(fminf(fminf(g0, g1), fminf(g2, g3)));
+      if (!(m <= r2)) break;
+      // the first slot holding the minimum; marked taken (+inf)
+      const uint64_t b0 = __ballot(g0 == m), b1 = __ballot(g1 == m), b2 = __ballot(g2 == m);
+      const uint32_t c = b0 ? (uint32_t)__builtin_ctzll(b0)
+                            : b1 ? 64u + (uint32_t)__builtin_ctzll(b1)
+                                 : b2 ? 128u + (uint32_t)__builtin_ctzll(b2)
+                                      : 192u + (uint32_t)__builtin_ctzll(__ballot(g3 == m));
+      if (l == (c & 63u)) {
+        const uint32_t slot = c >> 6;
+        g0 = slot == 0u ? __builtin_inff() : g0;
+        g1 = slot == 1u ? __builtin_inff() : g1;
+        g2 = slot == 2u ? __builtin_inff() : g2;
+        g3 = slot == 3u ? __builtin_inff() : g3;
+      }
+      const uint32_t q = (c * inx) >> 16, r = (q * iny) >> 16;
+      const CellLoad cl = fetch_cell(G, x0 + c - q * nx, y0 + q - r * ny, z0 + r);
+      if (have) {
+        process_cell<MODE>(s, G, pend, r2);
+        if (MODE == MODE_HIST) r2 = cull_r2<MODE>(s, G);
+        if (fbits(r2) == 0u) return true;
+      }
+      pend = cl;
+      have = true;
+    }
+    if (have) process_cell<MODE>(s, G, pend, r2);
+    return true;
+  }
   const uint32_t bx0 = cell_of(G.wlx, G.ox, G.scale, sh), bx1 = cell_of(G.whx, G.ox, G.scale, sh);
   const uint32_t by0 = cell_of(G.wly, G.oy, G.scale, sh), by1 = cell_of(G.why, G.oy, G.scale, sh);
   const uint32_t bz0 = cell_of(G.wlz, G.oz, G.scale, sh), bz1 = cell_of(G.whz, G.oz, G.scale, sh);
   const uint32_t lx = (uint32_t)G.lane & 3u, ly = ((uint32_t)G.lane >> 2) & 3u, lz = (uint32_t)G.lane >> 4;
-  CellLoad pend{0u, 0u, 0u, 0u, 0u};
-  bool have = false;
   for (int phase = 0; phase < 2; phase++) {
     const uint32_t ax = phase ? x0 : bx0, ay = phase ? y0 : by0, az = phase ? z0 : bz0;
     const uint32_t ex = phase ? x1 : bx1, ey = phase ? y1 : by1, ez = phase ? z1 : bz1;
@@ -507,6 +611,11 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   G.lane = lane;
   G.k = k;
   G.evals = G.cells_n = G.segs = 0;
+#ifdef LSK_GRID_PROFILE
+  for (int i = 0; i < 8; i++) G.prof[i] = 0;
+  G.ev_mode[0] = G.ev_mode[1] = 0;
+  LSK_GT(twave0);
+#endif
 
   Lane s;
   s.qx = valid ? A.qpts[3 * qi] : 0.f;
@@ -710,6 +819,19 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
     if (A.out_d2) A.out_d2[qi] = bitsf(s.lo_b);
     if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
   }
+#ifdef LSK_GRID_PROFILE
+  LSK_GADD(G.prof[7], twave0);
+  if (A.stats && lane == 0) {
+    // proc = processing; walk = pass total minus processing
+    atomicAdd(&A.stats[16], (unsigned long long)G.prof[0]);
+    atomicAdd(&A.stats[17], (unsigned long long)G.prof[1]);
+    atomicAdd(&A.stats[18], (unsigned long long)(G.prof[2] - G.prof[0]));
+    atomicAdd(&A.stats[19], (unsigned long long)(G.prof[3] - G.prof[1]));
+    atomicAdd(&A.stats[23], (unsigned long long)G.prof[7]);
+    atomicAdd(&A.stats[12], (unsigned long long)G.ev_mode[0]);
+    atomicAdd(&A.stats[13], (unsigned long long)G.ev_mode[1]);
+  }
+#endif
   if (A.stats) {
     auto cnt = [&](uint32_t bit) { return (unsigned long long)__popcll(__ballot(valid && (qs & bit))); };
     const unsigned long long c_ovf = cnt(QS_OVERFLOW), c_udf = cnt(QS_UNDERFLOW), c_ref = cnt(QS_REFINE),

@@ -54,7 +54,7 @@ class KnnConfig:
 # GPU indexes whose sub-cell populations look near-uniform (GRID_CROWD), "on" = always,
 # "off" = never (the bucket-tree kernel knn_rows serves every query).
 GRID = os.environ.get("LSKNN_GRID", "auto")
-GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "4"))  # target mean points per sub-cell
+GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "32"))  # target mean points per sub-cell
 # auto: a point's sub-cell holds on average at most this many times the mean (+1)
 GRID_CROWD = float(os.environ.get("LSKNN_GRID_CROWD", "3"))
 
@@ -136,7 +136,7 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
 
 def grid_level(distinct: list[int], n: int, ms: float = GRID_MS) -> int:
     """Sub-cell level of the grid: the finest level whose occupied sub-cells hold at least
-    `ms` points on average (uniform 1B points in a cube: 9, 1e8: 8, 1e7: 7), in [2, 10]."""
+    `ms` points on average (uniform 1B points in a cube: 8, 1e8: 7, 1e7: 6), in [2, 10]."""
     ls = 2
     for lvl in range(2, 11):
         if distinct[lvl] > 0 and n / distinct[lvl] >= ms:

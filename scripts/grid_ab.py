@@ -55,6 +55,13 @@ for impl in list(grids) + ["rows"]:
                      f" ovf {c.get('overflow_lanes', 0)} udf {c.get('underflow_lanes', 0)}"
                      f" refine {c.get('refine_lanes', 0)} cells/wave {c['leaves'] / c['waves']:.1f}"
                      f" segs/wave {c['nodes'] / c['waves']:.1f}")
+        if r == 0 and c.get("prof_wave"):
+            tot = c["prof_wave"]
+            extra += "\n    cycle profile (% of wave time): " + str(
+                {nm: round(100.0 * c.get("prof_" + nm, 0) / tot, 1)
+                 for nm in ("proc_hist", "proc_collect", "walk_hist", "walk_collect")})
+            if impl != "rows":
+                extra += f" evals/query hist {c['recorded_leaves'] / c['waves']:.0f} collect {c['collect_steps'] / c['waves']:.0f}"
         print(f"[{impl}] knn {n} pts k={a.k} ({a.dist}): {dt:.4f} s{extra}", flush=True)
     res[impl] = d2.clone()
 same = all(torch.equal(res[g].view(torch.int32), res["rows"].view(torch.int32)) for g in grids)
