@@ -354,6 +354,15 @@ __device__ __forceinline__ Batch load_batch(lsk::cfloat_p P, uint32_t i) {
 }
 constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0) (vmcnt / expcnt untouched)
 
+constexpr uint32_t kSegCheck = 1024;  // candidates between bound checks in a long segment
+
+template <int MODE>
+__device__ __forceinline__ void shrink_all(Lane &s, GridCtx &G) {
+  if (MODE == MODE_HIST && __ballot(s.state == ST_HIST && s.c_hi >= G.k)) {
+    if (s.state == ST_HIST && s.c_hi >= G.k) hist_shrink(s, G.pool, G.lane, G.k);
+  }
+}
+
 template <int MODE>
 __device__ __forceinline__ void eval4(Lane &s, GridCtx &G, const Batch &b) {
   const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
@@ -372,8 +381,16 @@ __device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0
   i1 = lsk::uniform(i1);
   uint32_t i = i0;
   Batch A = load_batch(P, i);
+  uint32_t chk = i0 + kSegCheck;
   for (;;) {  // A holds batch i (in flight)
     if (i + 4u > i1) break;
+    if (MODE == MODE_HIST && i >= chk) {
+      // long segment (a crowded sub-cell): once every lane's bound has closed (k exact
+      // copies: the k-th is 0) the rest of it cannot count
+      chk = i + kSegCheck;
+      shrink_all<MODE>(s, G);
+      if (!__ballot(s.state == ST_HIST && s.hi_b > 0u)) break;
+    }
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     Batch B = load_batch(P, i + 4u < i1 ? i + 4u : i);
     __builtin_amdgcn_sched_barrier(0);
@@ -398,18 +415,11 @@ __device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0
     const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
     update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane);
   }
-  G.evals += (i1 - i0 + 3u) & ~3u;
+  G.evals += (i1 - i0 + 3u) & ~3u;  // (an early stop counts the whole segment)
   G.segs++;
 #ifdef LSK_GRID_PROFILE
   G.ev_mode[MODE] += (i1 - i0 + 3u) & ~3u;
 #endif
-}
-
-template <int MODE>
-__device__ __forceinline__ void shrink_all(Lane &s, GridCtx &G) {
-  if (MODE == MODE_HIST && __ballot(s.state == ST_HIST && s.c_hi >= G.k)) {
-    if (s.state == ST_HIST && s.c_hi >= G.k) hist_shrink(s, G.pool, G.lane, G.k);
-  }
 }
 
 // Table entries of one level-lc cell, fetched ahead of use (vector loads: their counter
@@ -881,17 +891,31 @@ __global__ __launch_bounds__(256) void grid_build_kernel(const float *__restrict
 
 // counts[l] += number of i in [1, n) whose key prefix at level l (top 3l bits of the
 // 30-bit key) differs from key i-1's: distinct cells of level l = counts[l] + 1.
+// Grid-stride: per-thread counts in registers, wave sums, one atomic per level and block.
+constexpr int kLevelsBlocks = 1024;
 __global__ __launch_bounds__(256) void key_levels_kernel(const uint32_t *__restrict__ keys, int64_t n,
                                                          unsigned long long *__restrict__ counts) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool ok = i >= 1 && i < n;
-  const uint32_t a = ok ? keys[i - 1] : 0u, b = ok ? keys[i] : 0u;
-  const uint32_t x = a ^ b;  // differing bits
+  uint32_t c[11];
+#pragma unroll
+  for (int l = 0; l <= 10; l++) c[l] = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += stride) {
+    const uint32_t x = keys[i - 1] ^ keys[i];  // differing bits
+#pragma unroll
+    for (int l = 1; l <= 10; l++) c[l] += (x >> (3 * (10 - l))) != 0u ? 1u : 0u;
+  }
+  __shared__ uint32_t part[11][4];
+  const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int l = 1; l <= 10; l++) {
-    const bool d = ok && (x >> (3 * (10 - l))) != 0u;
-    const uint64_t m = __ballot(d);
-    if (lsk::lane_id() == 0 && m) atomicAdd(&counts[l], (unsigned long long)__popcll(m));
+    const uint32_t v = lsk::wave_sum(c[l]);
+    if (lsk::lane_id() == 0) part[l][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 1 && threadIdx.x <= 10) {
+    const int l = threadIdx.x;
+    const uint32_t v = part[l][0] + part[l][1] + part[l][2] + part[l][3];
+    if (v) atomicAdd(&counts[l], (unsigned long long)v);
   }
 }
 
@@ -937,7 +961,7 @@ extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long
   hipStream_t st = (hipStream_t)stream;
   LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
   if (n <= 1) return 0;
-  key_levels_kernel<<<lsk_blocks(n, 256), 256, 0, st>>>(keys, n, counts);
+  key_levels_kernel<<<lsk_blocks(n, 256, kLevelsBlocks), 256, 0, st>>>(keys, n, counts);
   LSK_CHECK_LAUNCH("key_levels");
   return 0;
 }

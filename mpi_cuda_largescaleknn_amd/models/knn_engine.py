@@ -56,7 +56,7 @@ class KnnConfig:
 GRID = os.environ.get("LSKNN_GRID", "auto")
 GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "32"))  # target mean points per sub-cell
 # auto: a point's sub-cell holds on average at most this many times the mean (+1)
-GRID_CROWD = float(os.environ.get("LSKNN_GRID_CROWD", "3"))
+GRID_CROWD = float(os.environ.get("LSKNN_GRID_CROWD", "2"))
 
 
 @dataclass
@@ -135,13 +135,27 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
 
 
 def grid_level(distinct: list[int], n: int, ms: float = GRID_MS) -> int:
-    """Sub-cell level of the grid: the finest level whose occupied sub-cells hold at least
-    `ms` points on average (uniform 1B points in a cube: 8, 1e8: 7, 1e7: 6), in [2, 10]."""
-    ls = 2
+    """Sub-cell level of the grid: the level whose occupied sub-cells hold closest to `ms`
+    points on average, in log scale (uniform points in a cube, ms = 32: 1B -> 8 (60 per
+    sub-cell), 1e8 -> 7 (48), 2e7 -> 6 (76), 1e7 -> 6 (38)), in [2, 10]. Measured best on
+    uniform data, k = 100 and 16 (scripts/grid_ab.py): coarse sub-cells cost more
+    candidates, fine ones more cells and segments."""
+    best, err = 2, math.inf
     for lvl in range(2, 11):
-        if distinct[lvl] > 0 and n / distinct[lvl] >= ms:
-            ls = lvl
-    return ls
+        if distinct[lvl] <= 0:
+            continue
+        e = abs(math.log(max(n / distinct[lvl], 1e-9) / ms))
+        if e < err:
+            best, err = lvl, e
+    return best
+
+
+def grid_applies(distinct: list[int], n: int, ls: int) -> bool:
+    """GRID=auto: near-uniform 3-D data at the grid's scale — occupied cells multiply by
+    >= 6 from level ls-1 to ls (planar data: 4, exact copies: 1), and the level's mean
+    population is within [4, 256] points."""
+    mean = n / max(1, distinct[ls])
+    return distinct[ls] >= 6 * distinct[ls - 1] and 4.0 <= mean <= 256.0
 
 
 def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
@@ -154,6 +168,8 @@ def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
         return None
     distinct = K.key_levels(skeys[:n])
     ls = grid_level(distinct, n)
+    if GRID == "auto" and not grid_applies(distinct, n, ls):
+        return None
     cells, subs = K.grid_build(index.pts, n, index.box, ls - 1)
     if GRID == "auto":
         seen = K.grid_sq(subs) / n          # mean population of a point's own sub-cell
