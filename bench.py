@@ -19,18 +19,21 @@ points): a stream of point sets — two different synthetic sets alternate step 
 step i runs its k-NN on the compute stream, step i+1's points are copied host -> device
 (PCIe H2D does not compete with the VALU-bound k-NN). Every step still uploads, builds, queries and
 returns its whole set; the first set's upload is inside the timed region, and both sets'
-last outputs are verified. ms_per_step is then the per-set time of the stream; the
-instrumented step below gives the single-set latency.
+last outputs are verified. ms_per_step is then the per-set time of the stream.
 
-After the timed region (untimed): one instrumented step of the timed path (per-phase
-times, max over ranks; halo sizes; per-rank k-NN ms; pipelined: from device-resident
-points) and a brute-force check of 256 sampled outputs per verified set against all
-points (utils/verify.py, `sampled_exact`). Rank 0 prints one JSON line.
+After the timed region (untimed): a brute-force check of 256 sampled outputs per verified
+set against all points (utils/verify.py, `sampled_exact`); the SINGLE-SET LATENCY — one
+set from pinned host memory through H2D, index build, k-NN and results back in host
+memory, nothing overlapped with another set (the BASELINE.md clock for one problem; best
+of two runs, max over ranks; `single_set_ms` / `single_set_mpts`); and one instrumented
+step of the timed path (per-phase times with device syncs, max over ranks; halo sizes;
+per-rank k-NN ms; pipelined: from device-resident points). Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -83,8 +86,10 @@ def parse():
     ap.add_argument("--direct-out", type=int, default=-1,
                     help="1 = on one rank the k-NN kernel writes the distances straight into the "
                          "pinned host buffer over PCIe while it runs (no device-to-host copy after "
-                         "it); 0 = device buffer + copy; -1 (default) = 1 when k >= 48 (where the "
-                         "PCIe writes hide under the kernel, pipelines.direct_host_out_pays)")
+                         "it); 0 = device buffer + copy; -1 (default) = a lone set: 1 when k >= 48 "
+                         "(where the PCIe writes hide under the kernel, "
+                         "pipelines.direct_host_out_pays); the stream of sets: 0 (the copy runs "
+                         "on a side stream under the next set)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="1 = capture the whole single-rank step (H2D, index build, k-NN, results "
                          "to host) in one HIP graph after the warmup and replay it per step; "
@@ -253,7 +258,10 @@ def main():
     elif pipelined:
         # stream of sets (parallel/stream.py): set i+1's upload under set i's build and
         # k-NN; several ranks: set i's results to host under set i+1
-        runner = SetStream(comm, cfg, direct_out=direct)
+        # the stream keeps results in device memory and copies them to host on a side
+        # stream: the kernel's direct PCIe writes contend with the next set's upload (1B,
+        # k=100: 1319 vs 1373 ms per set); a lone set (single_set_ms) writes directly
+        runner = SetStream(comm, cfg, direct_out=bool(args.direct_out) if args.direct_out >= 0 else False)
 
         def run_steps(n):
             with trace.range("lsknn:steps"):
@@ -267,6 +275,7 @@ def main():
     comm.barrier()
     _sync(device)
     ncoll0 = comm.collectives()
+    calls0 = dict(getattr(comm, "calls", {}))
     t0 = time.perf_counter()
     if pipelined:
         run_steps(args.steps)
@@ -278,6 +287,8 @@ def main():
     elapsed = time.perf_counter() - t0
     # collective launches of the timed steps (the closing barrier excluded)
     coll_per_step = (comm.collectives() - ncoll0 - (1 if comm.distributed else 0)) / max(1, args.steps)
+    calls = {op: round((c - calls0.get(op, 0)) / max(1, args.steps), 2)
+             for op, c in getattr(comm, "calls", {}).items() if op != "*" and c != calls0.get(op, 0)}
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.allreduce_(t, "max")
     elapsed = float(t.item())
@@ -304,6 +315,21 @@ def main():
             check = c if check is None else {"samples": check["samples"] + c["samples"],
                                              "exact": check["exact"] + c["exact"],
                                              "mismatch_ids": check["mismatch_ids"] + c["mismatch_ids"]}
+    # single-set latency: one set from pinned host memory to distances in host memory
+    # (the default non-streamed path of this variant), best of two, max over ranks
+    single_s = None
+    if args.mode == "halo" and device.type == "cuda":
+        best = math.inf
+        for _ in range(2):
+            comm.barrier()
+            _sync(device)
+            t1 = time.perf_counter()
+            _step(phases=False)
+            _sync(device)
+            best = min(best, time.perf_counter() - t1)
+        tt = torch.tensor([best], dtype=torch.float64, device=device)
+        comm.allreduce_(tt, "max")
+        single_s = float(tt.item())
     # the instrumented step takes the timed path: pipelined steps start from points already
     # on the device (their upload ran under the previous step), so this one does too
     pts_dev = host_pts.to(device) if pipelined else None
@@ -326,6 +352,8 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "single_set_ms": round(single_s * 1e3, 3) if single_s else None,
+            "single_set_mpts": round(n_total / single_s / 1e6, 3) if single_s else None,
             "dtype": "fp32",
             "data": "synthetic uniform-random float3 in [0,1)^3 (pinned host memory), no file I/O"
                     + ("; two different point sets alternate step by step" if pipelined else ""),
@@ -347,7 +375,7 @@ def main():
                 "all_finite": finite,
                 "sampled_exact": (f"{check['exact']}/{check['samples']}" if check else None),
             },
-            "detail": dict(detail, sampled_exact=check),
+            "detail": dict(detail, sampled_exact=check, comm_calls_per_step=calls),
         }
         print(json.dumps(rec), flush=True)
     LA.finalize(launch)

@@ -920,19 +920,25 @@ __global__ __launch_bounds__(256) void key_levels_kernel(const uint32_t *__restr
 }
 
 // sum over sub-cells of (end - start)^2: the mean sub-cell population seen by a point is
-// this / n (uniform data: about the mean population + 1).
+// this / n (uniform data: about the mean population + 1). Grid-stride, one atomic per block.
 __global__ __launch_bounds__(256) void grid_sq_kernel(const uint32_t *__restrict__ subs, int64_t nsub,
                                                       unsigned long long *__restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long v = 0;
-  if (i < nsub) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsub; i += stride) {
     const uint32_t a = subs[2 * i], b = subs[2 * i + 1];
     const unsigned long long d = b > a ? (unsigned long long)(b - a) : 0ull;
-    v = d * d;
+    v += d * d;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  if (lsk::lane_id() == 0 && v) atomicAdd(out, v);
+  __shared__ unsigned long long part[4];
+  if (lsk::lane_id() == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(out, t);
+  }
 }
 
 }  // namespace
@@ -970,7 +976,7 @@ extern "C" int lsk_hip_grid_sq(const uint32_t *subs, int64_t nsub, unsigned long
   hipStream_t st = (hipStream_t)stream;
   LSK_HIP(hipMemsetAsync(out, 0, sizeof(unsigned long long), st));
   if (nsub <= 0) return 0;
-  grid_sq_kernel<<<lsk_blocks(nsub, 256), 256, 0, st>>>(subs, nsub, out);
+  grid_sq_kernel<<<lsk_blocks(nsub, 256, kLevelsBlocks), 256, 0, st>>>(subs, nsub, out);
   LSK_CHECK_LAUNCH("grid_sq");
   return 0;
 }

@@ -436,14 +436,19 @@ def tree_set_radii_ub(nodes: torch.Tensor, pts: torch.Tensor, n: int, k: int) ->
     return nodes
 
 
-def halo_mask(pts: torch.Tensor, pub: torch.Tensor, pub_off: list[int], pub_depth: list[int], self_rank: int) -> torch.Tensor:
-    """Per point bitmask of ranks whose published radius-inflated boxes contain it."""
+def halo_mask(pts: torch.Tensor, pub: torch.Tensor, pub_off: list[int], pub_depth, self_rank: int) -> torch.Tensor:
+    """Per point bitmask of ranks whose published radius-inflated boxes contain it.
+    pub_depth: published tree depth per rank (list, or an int32 tensor — a device tensor
+    keeps the GPU path free of a host read)."""
     n = pts.shape[0]
     nranks = len(pub_off)
     mask = torch.empty(n, dtype=torch.int64, device=pts.device)
+    if isinstance(pub_depth, torch.Tensor) and not (is_gpu(pts) and pub_depth.device == pts.device):
+        pub_depth = [int(x) for x in pub_depth.cpu().tolist()]
     if is_gpu(pts):
         off = torch.tensor(pub_off, dtype=torch.int64, device=pts.device)
-        dep = torch.tensor(pub_depth, dtype=torch.int32, device=pts.device)
+        dep = (pub_depth.to(torch.int32).contiguous() if isinstance(pub_depth, torch.Tensor)
+               else torch.tensor(pub_depth, dtype=torch.int32, device=pts.device))
         check(_native.hip().lsk_hip_halo_mask(_ptr(pts), n, _ptr(pub), _ptr(off), _ptr(dep), nranks,
                                               self_rank, _ptr(mask), _stream(pts)), "halo_mask")
         return mask

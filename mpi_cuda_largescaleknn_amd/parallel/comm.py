@@ -72,6 +72,14 @@ class Comm:
         raise NotImplementedError
 
     # convenience -----------------------------------------------------------------
+    def count_exchange(self, counts: torch.Tensor) -> tuple[list[int], list[int]]:
+        """`counts` ([size] ints, device or host: this rank's rows for each rank) ->
+        (send counts, recv counts) on the host, through one all-gather of the count
+        vectors and ONE host read of the [size, size] matrix (the alternative, reading
+        the local counts and then exchanging them, costs two host round trips)."""
+        m = self.allgather(counts.reshape(-1).to(torch.int64)).cpu()
+        return [int(x) for x in m[self.rank]], [int(x) for x in m[:, self.rank]]
+
     def exchange_counts(self, send_counts: Sequence[int]) -> list[int]:
         t = torch.tensor(list(send_counts), dtype=torch.int64)
         allc = self.allgather_host(t)

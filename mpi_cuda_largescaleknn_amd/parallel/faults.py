@@ -79,7 +79,8 @@ class MonitoredComm(Comm):
     """Wraps a Comm: beats the heartbeat around every call and injects the configured
     fault (if any) on this rank."""
 
-    _OPS = ("allreduce_", "allgather", "alltoallv", "barrier", "p2p", "exchange_counts", "allgather_host")
+    _OPS = ("allreduce_", "allgather", "alltoallv", "barrier", "p2p", "exchange_counts", "allgather_host",
+            "count_exchange")
 
     def __init__(self, inner: Comm, fault: dict | None = None):
         self.inner = inner
@@ -136,6 +137,9 @@ class MonitoredComm(Comm):
 
     def exchange_counts(self, counts):
         return self._call("exchange_counts", counts)
+
+    def count_exchange(self, counts):
+        return self._call("count_exchange", counts)
 
     def allgather_host(self, t):
         return self._call("allgather_host", t)

@@ -178,9 +178,9 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
     splitters = _splitters(hist_h, total, size)
     perm, counts = _dest_and_perm(keys, splitters, size)
     send = K.gather3(points, perm)
-    send_counts = counts.cpu().tolist()
+    send_counts, recv_counts = comm.count_exchange(counts)  # one host read
     info.timer.mark("partition")
-    recv, recv_counts = comm.alltoallv(send, send_counts)
+    recv, recv_counts = comm.alltoallv(send, send_counts, recv_counts)
     info.timer.mark("alltoallv_points")
     info.counts["sent_points"] = sum(send_counts) - send_counts[comm.rank]
     info.counts["owned_points"] = int(recv.shape[0])
@@ -284,8 +284,8 @@ def redistribute_stream(host_pts: torch.Tensor, comm: Comm, info: RunInfo,
         keys_c = keys0 if c == 0 else K.morton(pts_c, box0, with_iota=False)[0]
         perm_c, counts_c = _dest_and_perm(keys_c, splitters, size)
         send_c = K.gather3(pts_c, perm_c)
-        sc = counts_c.cpu().tolist()
-        recv_c, rc = comm.alltoallv(send_c, sc)
+        sc, rc = comm.count_exchange(counts_c)  # one host read per chunk
+        recv_c, rc = comm.alltoallv(send_c, sc, rc)
         recvs.append(recv_c)
         rcs.append(rc)
         perms.append(perm_c)
@@ -392,21 +392,23 @@ def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: 
     pub[:, 4:7] = -math.inf
     take = min(rows, radii_nodes.shape[0], 2 << my_levels)
     pub[:take] = radii_nodes[:take]
-    meta = torch.tensor([my_levels], dtype=torch.int32, device=dev)
+    # the published depth rides in node 0's unused hi.w: one all-gather, no host read
+    pub[0, 7] = float(my_levels)
     pub_all = comm.allgather(pub)                       # [P, rows, 8]
-    depths = comm.allgather(meta).view(-1).cpu().tolist()
+    depths = pub_all[:, 0, 7].to(torch.int32)           # (device)
     if marks:
         info.timer.mark("halo_publish")
     pts = index.pts[:n]
     offs = [j * rows * 8 for j in range(size)]
     mask = K.halo_mask(pts, pub_all.reshape(-1), offs, depths, rank)
+    recv_counts = None
     if K.is_gpu(pts):
         from .. import _native
         lib = _native.hip()
         counts = torch.zeros(size, dtype=torch.int32, device=dev)
         K.check(lib.lsk_hip_mask_counts(mask.data_ptr(), n, size, counts.data_ptr(), K._stream(pts)),
                 "mask_counts")
-        send_counts = counts.cpu().tolist()
+        send_counts, recv_counts = comm.count_exchange(counts)  # one host read
         offsets = [0]
         for c in send_counts:
             offsets.append(offsets[-1] + c)
@@ -424,7 +426,7 @@ def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: 
         send = torch.cat(parts) if parts else pts[:0]
     if marks:
         info.timer.mark("halo_filter")
-    recv, _ = comm.alltoallv(send, send_counts)
+    recv, _ = comm.alltoallv(send, send_counts, recv_counts)
     info.counts["halo_sent"] = int(sum(send_counts))
     info.counts["halo_recv"] = int(recv.shape[0])
     if marks:

@@ -29,27 +29,49 @@ from .comm import Comm
 from .pipelines import PhaseTimer, RunInfo
 
 
-def ring_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None) -> torch.Tensor:
+def ring_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
+             overlap: bool = True) -> torch.Tensor:
+    """Ring rotation (unorderedDataVariant.cu:173-205), double-buffered: the tree sizes
+    are all-gathered once up front (the reference exchanges one count per round,
+    :183-187 — the same numbers), and round r+1's tree exchange (send the tree held in
+    round r to rank+1, receive rank-1's into the other buffer) is posted on a
+    high-priority side stream before round r's query is launched, so the xGMI transfer
+    runs under the k-NN kernel (the reference waits for each exchange, D6). `overlap`
+    False: the reference's sequential order (same results)."""
     info = info or RunInfo(PhaseTimer(False, points.device))
     info.timer.start()
     points = points.contiguous()
     n = points.shape[0]
     dev = points.device
+    size, rank = comm.size, comm.rank
     tree, _ = R.build_lbt(points)
     info.timer.mark("build")
     heaps = R.alloc_heaps(n, cfg.k, dev)
-    nxt, prv = (comm.rank + 1) % comm.size, (comm.rank - 1 + comm.size) % comm.size
+    counts = comm.allgather(torch.tensor([n], dtype=torch.int64, device=comm.device)).view(-1).cpu().tolist()
+    nxt, prv = (rank + 1) % size, (rank - 1 + size) % size
+    gpu = dev.type == "cuda"
+    side = torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1]) if gpu and overlap else None
+    compute = torch.cuda.current_stream(dev) if gpu else None
     cur, cur_n = tree, n
-    for rnd in range(comm.size):
-        if rnd > 0:
-            cnt = torch.tensor([cur_n], dtype=torch.int64, device=comm.device)
-            (rc,) = comm.p2p([(nxt, cnt)], [(prv, (1,), torch.int64)])
-            recv_n = int(rc.item())
-            (cur,) = comm.p2p([(nxt, cur[:cur_n])], [(prv, (recv_n, 3), torch.float32)])
-            cur_n = recv_n
+    for rnd in range(size):
+        got = None
+        if rnd + 1 < size:
+            recv_n = counts[(rank - rnd - 1) % size]  # the tree rank-1 holds this round
+            if side is not None:
+                side.wait_stream(compute)  # `cur` complete (received / built) on the device
+                with torch.cuda.stream(side):
+                    (got,) = comm.p2p([(nxt, cur[:cur_n])], [(prv, (recv_n, 3), torch.float32)])
+                cur.record_stream(side)
+            else:
+                (got,) = comm.p2p([(nxt, cur[:cur_n])], [(prv, (recv_n, 3), torch.float32)])
             info.timer.mark("ring_exchange")
         R.run_query(cur, cur_n, points, heaps, cfg.k, cfg.cut2, init=(rnd == 0))
         info.timer.mark("knn_rounds")
+        if got is not None:
+            if side is not None:
+                compute.wait_stream(side)  # round r+1 reads the received tree
+                got.record_stream(compute)
+            cur, cur_n = got, recv_n
     out = R.extract(heaps, n, cfg.k)
     info.timer.mark("return")
     return out

@@ -97,6 +97,10 @@ class SetStream:
         cur = torch.cuda.current_stream(self.device)
         if n:
             self._prefetch(0, inputs[0])
+        # no host sync between sets: set i+1's build is queued right behind set i's k-NN
+        # (the stream orders them), and set i's failure-word read (a host sync, see
+        # knn_engine.query `deferred`) waits until set i+1's work is queued
+        pend: list = []
         for i in range(n):
             cur.wait_stream(self.copy_stream)  # set i's points are on the device
             pts = self._dbuf[i % 2]
@@ -104,13 +108,22 @@ class SetStream:
                 self._prefetch(i + 1, inputs[i + 1])
             info = new_info()
             with trace.range(f"lsknn:set {i}"):
-                res = PL.unordered_knn(pts, self.comm, self.cfg, info, n_total=n_totals[i],
-                                       out=outputs[i] if self.direct_out else None)
+                info.timer.start()
+                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info)
+                E.settle(pend)  # set i-1's failure word: its k-NN ran before this build
+                direct = self.direct_out
+                res = PL.local_query(index, hint2, self.cfg, info, outputs[i] if direct else None,
+                                     deferred=pend)
                 if res.data_ptr() != outputs[i].data_ptr():
-                    outputs[i].copy_(res, non_blocking=True)
-                del res
-                torch.cuda.synchronize(self.device)
+                    # device results: their copy to host runs on a side stream under the
+                    # next set's build and k-NN
+                    self.out_stream.wait_stream(cur)
+                    with torch.cuda.stream(self.out_stream):
+                        outputs[i].copy_(res, non_blocking=True)
+                    res.record_stream(self.out_stream)
+                del res, index
             self.last_info = info
+        E.settle(pend)
         torch.cuda.synchronize(self.device)  # the last results are in host memory
 
     def _run_distributed(self, inputs, outputs, n_totals, new_info) -> None:

@@ -64,13 +64,16 @@ def test_refalgo_large_k_64bit_offsets():
 
 
 @pytest.mark.parametrize("size", [2, 4])
-def test_ring_multirank_gpu(size):
+@pytest.mark.parametrize("overlap", [True, False])
+def test_ring_multirank_gpu(size, overlap):
+    """Double-buffered ring (next round's exchange on a side stream under the query) and
+    the reference's sequential order give the same bits as one rank."""
     p = uniform(50_000, seed=size)
     k = 32
 
     def fn(comm):
         b, e = p.shape[0] * comm.rank // comm.size, p.shape[0] * (comm.rank + 1) // comm.size
-        return RA.ring_knn(p[b:e].to(DEV), comm, E.KnnConfig(k=k)).cpu()
+        return RA.ring_knn(p[b:e].to(DEV), comm, E.KnnConfig(k=k), overlap=overlap).cpu()
 
     out = torch.cat(run_loopback(size, fn, DEV))
     assert torch.equal(out, E.knn_distances(p.to(DEV), k).cpu())
