@@ -246,6 +246,7 @@ def main():
         _sync(device)
         # over-full key cells seen by the eager warmup: capture the (fixed-size) refinement
         E.REFINE_CAPTURE = E.LAST_REFINED
+        E.prepare_capture(device)  # failure-word peaks over every replay
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             _step()
@@ -297,7 +298,7 @@ def main():
     value = n_total * args.steps / elapsed / 1e6
     heavy_unrefined = False
     if graph is not None:
-        E.verify_captured_failures(clear=True)  # raises if a replay overflowed a failure list
+        E.verify_captured_failures(clear=True)  # raises if any replay overflowed a failure list
         heavy_unrefined = E.captured_heavy_cells(clear=True)
     # the sets the timed steps wrote last (pipelined: both sets when K >= 2)
     written = sorted({(args.steps - 1 - j) % len(host_sets) for j in range(min(args.steps, len(host_sets)))})

@@ -13,6 +13,7 @@
 //   `max_piece` bytes go in pieces: MPI counts are int), bcast, barrier, abort.
 // Each call is blocking and returns 0, or non-zero with lsk_mpi_last_error() set.
 #include <mpi.h>
+#include <unistd.h>
 
 #include <climits>
 #include <cstdint>
@@ -93,13 +94,22 @@ int lsk_mpi_abi_version() { return 1; }
 
 // MPI_Init_thread (SERIALIZED: collectives from the main thread, MPI_Abort from the
 // watchdog thread) unless MPI is already up; returns this rank's place in COMM_WORLD.
+// The watchdog thread may call lsk_mpi_abort while the main thread is inside an MPI call:
+// that needs MPI_THREAD_MULTIPLE. When the library grants less (or MPI was initialised by
+// someone else at a lower level), abort falls back to _exit: mpirun then tears down the
+// other ranks when this one disappears (lsk_mpi_abort).
+static bool g_thread_multiple = false;
+
 int lsk_mpi_init(int *rank, int *size) {
   int inited = 0;
   LSK_MPI(MPI_Initialized(&inited));
+  int provided = MPI_THREAD_SINGLE;
   if (!inited) {
-    int provided = 0;
-    LSK_MPI(MPI_Init_thread(nullptr, nullptr, MPI_THREAD_SERIALIZED, &provided));
+    LSK_MPI(MPI_Init_thread(nullptr, nullptr, MPI_THREAD_MULTIPLE, &provided));
+  } else {
+    LSK_MPI(MPI_Query_thread(&provided));
   }
+  g_thread_multiple = provided >= MPI_THREAD_MULTIPLE;
   // errors come back as return codes (reported through lsk_mpi_last_error), not aborts
   LSK_MPI(MPI_Comm_set_errhandler(MPI_COMM_WORLD, MPI_ERRORS_RETURN));
   LSK_MPI(MPI_Comm_rank(MPI_COMM_WORLD, rank));
@@ -116,8 +126,15 @@ int lsk_mpi_finalize() {
 }
 
 // The reference's failure path: an MPI error ends the whole job (CUKD_MPI_CALL throws,
-// nothing catches, mpirun tears every rank down). Here: MPI_Abort on COMM_WORLD.
-void lsk_mpi_abort(int code) { MPI_Abort(MPI_COMM_WORLD, code); }
+// nothing catches, mpirun tears every rank down). Here: MPI_Abort on COMM_WORLD when MPI
+// allows a second thread inside it (the watchdog calls this while the main thread may be
+// blocked in a collective), else _exit — the launcher ends the other ranks.
+void lsk_mpi_abort(int code) {
+  if (g_thread_multiple) MPI_Abort(MPI_COMM_WORLD, code);
+  _exit(code ? code : 1);
+}
+
+int lsk_mpi_thread_multiple() { return g_thread_multiple ? 1 : 0; }
 
 int lsk_mpi_barrier() {
   LSK_MPI(MPI_Barrier(MPI_COMM_WORLD));

@@ -34,8 +34,18 @@ SEED_BUCKETS = 1  # curve-neighbour buckets (each side) that seed the first pass
 KNN_IMPL = "rows"  # "rows" (production kernel + exact backstop) or "exact" (backstop only)
 DEBUG_FAIL_MOD = 0  # tests: make the rows kernel hand every m-th query to the backstop
 # HIP-graph captures: the failure words of captured launches, checked after a replay
-# (verify_captured_failures) — during a capture the host cannot read them
+# (verify_captured_failures) — during a capture the host cannot read them. A replay
+# re-zeroes each launch's counter, so every captured launch also folds its count into a
+# peak slot of CAPTURE_PEAKS (allocated and zeroed by prepare_capture, outside the graph):
+# the check then covers every replay, not only the last one.
 CAPTURED_FAIL_WORDS: list = []
+CAPTURE_PEAKS: torch.Tensor | None = None
+
+
+def prepare_capture(device: torch.device, slots: int = 64) -> None:
+    """Call before capturing k-NN launches into a graph (see CAPTURED_FAIL_WORDS)."""
+    global CAPTURE_PEAKS
+    CAPTURE_PEAKS = torch.zeros(slots, dtype=torch.int64, device=device)
 
 
 @dataclass
@@ -383,6 +393,10 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
             stats.add(raw)
 
     if torch.cuda.is_current_stream_capturing():
+        slot = len(CAPTURED_FAIL_WORDS)
+        if fw.count is not None and CAPTURE_PEAKS is not None and slot < CAPTURE_PEAKS.numel():
+            fw.peak = CAPTURE_PEAKS[slot:slot + 1]
+            torch.maximum(fw.peak, fw.count.to(torch.int64) & 0xFFFFFFFF, out=fw.peak)
         CAPTURED_FAIL_WORDS.append(fw)
         if stats is not None:
             stats.add(raw)
@@ -408,6 +422,9 @@ def verify_captured_failures(clear: bool = False) -> int:
     total = 0
     for fw in CAPTURED_FAIL_WORDS:
         v = fw.value()
+        peak = getattr(fw, "peak", None)
+        if peak is not None:
+            v = max(v, int(peak.item()))  # the worst replay
         if v > fw.cap:
             raise RuntimeError(f"k-NN failure list overflow in a captured graph ({v} > {fw.cap}): "
                                "rerun eagerly")

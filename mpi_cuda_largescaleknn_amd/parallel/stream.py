@@ -75,25 +75,34 @@ class SetStream:
 
     def run(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor],
             n_totals: Sequence[int | None] | None = None,
-            info_factory: Callable[[], PL.RunInfo] | None = None) -> None:
+            info_factory: Callable[[], PL.RunInfo] | None = None,
+            on_done: Callable[[int], None] | None = None) -> None:
         """Set i: this rank's points inputs[i] (pinned host memory for GPU runs) ->
         distances in outputs[i] (float32, one per point, pinned for GPU runs). Returns
         when every output is in host memory. `n_totals[i]`: the set's global point count
-        (None: summed over ranks)."""
+        (None: summed over ranks).
+
+        `inputs` / `outputs` are only indexed (in set order, a set or two ahead), so they
+        may be lazy sequences that read / allocate on first access. `on_done(i)` is called
+        once outputs[i] is complete in host memory and inputs[i] is no longer read — a
+        caller can write the result and release both buffers there, so a long stream keeps
+        only ~3 sets alive (apps/stream.py)."""
         n = len(inputs)
         if len(outputs) != n:
             raise ValueError("SetStream.run: one output per input")
         n_totals = list(n_totals) if n_totals is not None else [None] * n
         new_info = info_factory or (lambda: PL.RunInfo(PL.PhaseTimer(False, self.device)))
+        done = on_done or (lambda i: None)
         if not self.gpu:
             for i in range(n):
                 info = new_info()
                 out = PL.unordered_knn(inputs[i], self.comm, self.cfg, info, n_total=n_totals[i])
                 outputs[i].copy_(out)
                 self.last_info = info
+                done(i)
             return
         if self.comm.distributed:
-            return self._run_distributed(inputs, outputs, n_totals, new_info)
+            return self._run_distributed(inputs, outputs, n_totals, new_info, done)
         cur = torch.cuda.current_stream(self.device)
         if n:
             self._prefetch(0, inputs[0])
@@ -101,6 +110,7 @@ class SetStream:
         # (the stream orders them), and set i's failure-word read (a host sync, see
         # knn_engine.query `deferred`) waits until set i+1's work is queued
         pend: list = []
+        fin: list = []  # (set, event after which its output is in host memory)
         for i in range(n):
             cur.wait_stream(self.copy_stream)  # set i's points are on the device
             pts = self._dbuf[i % 2]
@@ -114,19 +124,30 @@ class SetStream:
                 direct = self.direct_out
                 res = PL.local_query(index, hint2, self.cfg, info, outputs[i] if direct else None,
                                      deferred=pend)
+                ev = torch.cuda.Event()
                 if res.data_ptr() != outputs[i].data_ptr():
                     # device results: their copy to host runs on a side stream under the
                     # next set's build and k-NN
                     self.out_stream.wait_stream(cur)
                     with torch.cuda.stream(self.out_stream):
                         outputs[i].copy_(res, non_blocking=True)
+                        ev.record(self.out_stream)
                     res.record_stream(self.out_stream)
+                else:
+                    ev.record(cur)
                 del res, index
             self.last_info = info
+            fin.append((i, ev))
+            while len(fin) > 1:  # set i-1 (queued before set i's work) is retired
+                j, e = fin.pop(0)
+                e.synchronize()
+                done(j)
         E.settle(pend)
         torch.cuda.synchronize(self.device)  # the last results are in host memory
+        for j, _ in fin:
+            done(j)
 
-    def _run_distributed(self, inputs, outputs, n_totals, new_info) -> None:
+    def _run_distributed(self, inputs, outputs, n_totals, new_info, done) -> None:
         comm, cfg, dev = self.comm, self.cfg, self.device
         cur = torch.cuda.current_stream(dev)
         redist = self.redist_stream
@@ -138,6 +159,7 @@ class SetStream:
                 n_totals[j] = int(t.item())
         if n == 0:
             return
+        fin: list = []
         self._prefetch(0, inputs[0])
         cur.wait_stream(self.copy_stream)
         P = PL.redistribute_set(self._dbuf[0], comm, cfg, n_totals[0], new_info())
@@ -159,8 +181,10 @@ class SetStream:
             with trace.range(f"lsknn:set {i}"):
                 res = PL.compute_set(P, comm, cfg, info, hook=hook if i + 1 < n else None)
             self.out_stream.wait_stream(cur)
+            ev = torch.cuda.Event()
             with torch.cuda.stream(self.out_stream):
                 outputs[i].copy_(res, non_blocking=True)
+                ev.record(self.out_stream)
             res.record_stream(self.out_stream)  # kept until its copy is done
             del res
             cur.synchronize()
@@ -170,4 +194,11 @@ class SetStream:
             cur.wait_stream(redist)
             P = nxt.get("P")
             self.last_info = info
+            fin.append((i, ev))
+            while len(fin) > 1:  # set i-1's copy was queued before set i's
+                j, e = fin.pop(0)
+                e.synchronize()
+                done(j)
         torch.cuda.synchronize(dev)  # the last results are in host memory
+        for j, _ in fin:
+            done(j)

@@ -98,3 +98,56 @@ def test_compute_set_hook_redistributes_next_set_cpu(size):
     outs = run_loopback(size, fn)
     assert torch.equal(torch.cat([o[0] for o in outs]), oracle(A, k))
     assert torch.equal(torch.cat([o[1] for o in outs]), oracle(B, k))
+
+
+class _Lazy:
+    """A lazily materialised sequence that records accesses and what is alive."""
+
+    def __init__(self, make, n):
+        self.make, self.n, self.alive, self.log = make, n, {}, []
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        if i not in self.alive:
+            self.alive[i] = self.make(i)
+            self.log.append(i)
+        return self.alive[i]
+
+
+def _check_lazy_stream(dev, pin, direct):
+    k = 12
+    S = sets() * 2
+    ins = _Lazy(lambda i: S[i].pin_memory() if pin else S[i].clone(), len(S))
+    outs = _Lazy(lambda i: torch.full((S[i].shape[0],), -1.0).pin_memory() if pin
+                 else torch.full((S[i].shape[0],), -1.0), len(S))
+    done, peak = [], [0]
+
+    def on_done(i):
+        assert torch.equal(outs[i], oracle(S[i], k)), i
+        done.append(i)
+        ins.alive.pop(i)
+        outs.alive.pop(i)
+
+    def track(i):
+        peak[0] = max(peak[0], len(ins.alive))
+
+    ins_get = ins.__getitem__
+    ins.__class__ = type("_LazyTracked", (_Lazy,), {"__getitem__": lambda self, i: (ins_get(i), track(i))[0]})
+    SetStream(SingleComm(dev), E.KnnConfig(k=k), direct_out=direct).run(ins, outs, on_done=on_done)
+    assert done == list(range(len(S)))
+    assert not ins.alive and not outs.alive
+    assert peak[0] <= 3  # only the sets in flight are materialised
+
+
+def test_stream_lazy_sets_and_on_done_cpu():
+    """Sets are read when reached and released in on_done (apps/stream.py's bounded host
+    memory): callbacks in order, every output complete when its callback runs."""
+    _check_lazy_stream(torch.device("cpu"), False, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direct", [True, False])
+def test_stream_lazy_sets_and_on_done_gpu(direct):
+    _check_lazy_stream(torch.device("cuda", torch.cuda.current_device()), True, direct)
