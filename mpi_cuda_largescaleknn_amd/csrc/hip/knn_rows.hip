@@ -1,17 +1,29 @@
-// k-th-NN distance selection, row-decomposed variant (the production kernel).
+// k-th-NN distance selection over the bucket tree (knn_rows_kernel): the tree-walk k-NN
+// pass — the path for skewed data (clustered, planar, exact copies, mixed scale) and for
+// halo re-queries against two trees; near-uniform local passes use knn_grid.hip, which
+// shares the selection algorithm below. Contract: reference runQuery +
+// extractFinalResult (unorderedDataVariant.cu:75-103): for every query, the k-th smallest
+// canonical squared distance (common.h dist2) to the tree points, self included, or the
+// cutoff when fewer than k points lie below it.
 //
-// Same contract and selection algorithm as knn.hip (two-pass radix select on d² bits
-// with a per-lane LDS histogram, LDS collect pool and per-lane (k-c_lo)-max-heap; see the
-// header of knn.hip and the reference runQuery/extractFinalResult,
-// unorderedDataVariant.cu:75-103), with a different SIMD decomposition:
+// Selection: a radix select on the float bits of d² (non-negative floats order like their
+// bits). Pass 1 (HIST) counts each lane's values in 40 bins of 1/8 octave of d² in LDS
+// (two 16-bit counters per dword) over a range placed by an estimate of the k-th value;
+// the range top shrinks online as soon as k values lie below a bin edge, which is what
+// culls the walk. Pass 2 (COLLECT) gathers the values of the bin holding the k-th into a
+// per-wave LDS pool, where a per-lane (k - below)-max-heap yields the exact value. Lanes
+// whose range was wrong (overflow / underflow / too-full bin) run further passes; lanes
+// the 16-bit counters cannot resolve exactly go to the failure list (knn_exact.hip).
 //
-//  * a wave owns 64 consecutive Morton-sorted queries split into 4 ROWS of 16 (the
-//    16-lane rows of CDNA4 DPP). The tree walk is wave-uniform (DFS with the stack in one
-//    VGPR, 4-ary steps over the implicit bucket tree, scalar node loads, near child
-//    first); at the level above the buckets each row tests the 8 16-point QUARTER boxes
-//    of the node's two buckets with its own 16 lanes and queues the quarters it needs.
-//    Quarter boxes of 4 such nodes are fetched with one vector load per node (one
-//    memory latency per batch) and broadcast with v_readlane;
+// SIMD decomposition:
+//  * a wave owns 64 consecutive Hilbert-sorted queries split into 4 ROWS of 16 (the
+//    16-lane rows of CDNA4 DPP). The tree walk is wave-uniform: best-first over the
+//    implicit bucket tree (64-entry priority list in two VGPRs, DFS stack in one VGPR as
+//    bounded overflow, 4-ary steps with scalar node loads); at the level above the
+//    buckets each row tests the 8 16-point QUARTER boxes of the node's two buckets with
+//    its own 16 lanes and queues the quarters it needs. Quarter boxes of 4 such nodes are
+//    fetched with one vector load per node (one memory latency per batch) and broadcast
+//    with v_readlane;
 //  * rows consume their queues in lockstep: one step = one quarter per row, the 16
 //    candidates of each row's quarter are loaded by the row's 16 lanes (one vector load,
 //    prefetched one step ahead) and broadcast inside the row with DPP row_newbcast, which
@@ -26,7 +38,7 @@
 //  * histogram bin index = sat(d²bits - lo) >> shift: values below the range land in bin
 //    0 (no separate compare), and c_base tracks how many of them are known to be below;
 //  * the per-lane estimate that places the first range is capped by the wave's lower
-//    quartile: groups straddling a Morton discontinuity otherwise produce a few waves
+//    quartile: groups straddling a curve discontinuity otherwise produce a few waves
 //    with absurd first-pass bounds that dominate the kernel's tail.
 //  Inner-loop cost per candidate and lane: 6 VALU for d² (DPP broadcast folded into the
 //  subtracts) + 5 VALU + 1 exec-masked ds_add for the histogram when in range (compiled

@@ -2,13 +2,14 @@
 
 Fast path ("halo" mode), shared by both entrypoints:
 
-1. (unordered only) spatial redistribution — global bounds (all-reduce), 30-bit Morton
-   keys in the global cube, global histogram of the top 16 key bits (all-reduce) ->
+1. (unordered only) spatial redistribution — global bounds (all-reduce), 30-bit Hilbert
+   curve keys in the global cube, global histogram of the top 16 key bits (all-reduce) ->
    P-1 balanced splitters, destination-rank partition (radix sort by rank), rows moved
    with all-to-all-v. This is the sequence-parallel/Ulysses-style reshard of SURVEY §5.7a
    and replaces the reference's P-round ring of whole trees (unorderedDataVariant.cu:
    173-205, P kNN passes per query, O(P) traffic).
-2. local index (Morton sort + bucket tree) and local k-NN on the owned points.
+2. local index (Hilbert sort + bucket tree + cell grid) and local k-NN on the owned
+   points (knn_grid.hip for near-uniform data, knn_rows.hip otherwise).
 3. halo exchange — each rank publishes the top levels of its tree with per-node max
    k-NN radius (all-gather, tiny); every rank sends exactly the points that fall
    inside another rank's radius-inflated boxes (halo_mask kernel, all-to-all-v); the
