@@ -5,7 +5,7 @@ build a k-d tree over the rank's points (cukd::buildTree, unorderedDataVariant.c
 and answer one k-NN query per point (runQuery/extractFinalResult, :75-103). Pipeline
 on the GPU — every step a hand-written gfx950 kernel on torch's current stream:
 
-    bounds -> Morton keys -> LSD radix sort -> gather -> bucket tree -> radix-select k-NN
+    bounds -> Hilbert keys -> LSD radix sort -> gather -> bucket tree (+ cell grid) -> radix-select k-NN
 
 ``LocalIndex`` is the reusable product of the first five steps (also used for the
 halo tree in the distributed pipelines).
@@ -86,12 +86,12 @@ class GridIndex:
 @dataclass
 class LocalIndex:
     n: int
-    pts: torch.Tensor        # [n + PAD, 3] Morton-sorted points (padded)
+    pts: torch.Tensor        # [n + PAD, 3] curve-sorted (Hilbert) points (padded)
     perm: torch.Tensor       # int32 [n]: sorted position -> row of the input array
     nodes: torch.Tensor      # [2^(depth+1), 8] bucket-tree node boxes (lo.w = radius²)
     qnodes: torch.Tensor     # [2^depth * 4, 8] boxes of each bucket's four 16-point quarters
     depth: int
-    box: torch.Tensor        # [8] cube used for the Morton keys
+    box: torch.Tensor        # [8] cube used for the curve keys
     grid: GridIndex | None = None
 
     @property

@@ -37,7 +37,7 @@ from ..utils import trace
 from .comm import Comm
 from .faults import HEARTBEAT
 
-SPLIT_BITS = 16  # splitter resolution: top 16 of the 30 Morton bits
+SPLIT_BITS = 16  # splitter resolution: top 16 of the 30 curve-key bits
 
 
 @dataclass
@@ -103,7 +103,7 @@ def _hist_sample(n: int) -> int:
 def _splitters(hist: torch.Tensor, total: int, size: int) -> list[int]:
     """Bin starts of ranks 1..P-1 so that each rank owns ~total/P points.
 
-    Each splitter is snapped to the coarsest Morton cell boundary (level m: 8^m cells,
+    Each splitter is snapped to the coarsest octree cell boundary (level m: 8^m cells,
     2^(SPLIT_BITS-3m) histogram bins) whose count stays within SPLIT_TOL of the ideal
     share. A rank range ending mid-cell owns a sliver of a distant cell; bucket-tree
     nodes spanning that Z-order jump have huge boxes and blow up the halo (uniform data,
@@ -159,7 +159,7 @@ def _dest_and_perm(keys: torch.Tensor, splitters: list[int], size: int):
 
 
 def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunInfo):
-    """Move every point to the rank owning its Morton range.
+    """Move every point to the rank owning its curve-key range.
     Returns (owned points, recv_counts, send permutation, send counts)."""
     size = comm.size
     keys, _ = K.morton(points, box, with_iota=False)
