@@ -90,8 +90,8 @@ class KnnArgs(C.Structure):
 
 class GridView(C.Structure):
     _fields_ = [
-        ("cells", vp),
-        ("subs", vp),
+        ("slots", vp),
+        ("pad_", vp),
         ("box", vp),
         ("inf4", vp),
         ("level", C.c_int32),
@@ -165,7 +165,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_knn_exact": ([C.POINTER(KnnArgs), vp, vp, i64, vp], i32),
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_knn_grid": ([C.POINTER(KnnArgs), C.POINTER(GridView), vp], i32),
-        "lsk_hip_grid_build": ([vp, i64, vp, i32, vp, vp, vp], i32),
+        "lsk_hip_grid_build": ([vp, vp, i64, vp, i32, vp, vp], i32),
         "lsk_hip_key_levels": ([vp, i64, vp, vp], i32),
         "lsk_hip_grid_sq": ([vp, i64, vp, vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),

@@ -6,27 +6,33 @@
 // backstop; reference runQuery / extractFinalResult, unorderedDataVariant.cu:75-103). What
 // differs is where the candidates come from and how they are broadcast:
 //
-//  * the Hilbert-sorted points are indexed by an octree grid at two levels: every cell of
-//    level `lc` and every one of its 8 sub-cells (level lc+1) is a contiguous run of the
-//    sorted array (an aligned block of Hilbert keys), stored as (start, end) pairs in
-//    Morton order of the cell coordinates (the 8 sub-cells of a cell are 8 consecutive
-//    entries). Built in one pass over the sorted points (grid_build_kernel);
-//  * a wave owns 64 curve-consecutive queries. A pass enumerates the cells around the
-//    wave's query box ARITHMETICALLY (cell coordinates from the quantised box ± the
-//    current radius; no pointer chasing, no priority queue): lane j tests cell j of the
-//    range against the box, the needed cells are taken in ballot order, the cells
-//    holding the queries first (their candidates shrink the histogram ranges early);
-//  * per cell, lanes 0-7 test its 8 sub-cells; a fully needed cell is one contiguous
-//    segment, otherwise every needed sub-cell is one;
-//  * a segment's points are read with SCALAR loads (wave-uniform addresses through the
-//    constant address space): the candidates arrive in SGPRs and every VALU op of the
-//    canonical d² takes them as an operand — 6 VALU per candidate and lane, no
-//    broadcast, no per-row queues or logs. The per-lane bound only shrinks during a pass,
-//    and the cull radius follows it cell by cell.
+//  * the curve-sorted points are indexed by an octree grid: every cell of level `lc` has
+//    64 slots, one per grandchild (level lc+2) IN CURVE ORDER — which is memory order —
+//    holding the grandchild's contiguous run of the sorted array and its coordinates.
+//    Built in one pass over the sorted points and keys (grid_build_kernel: a grandchild's
+//    slot is the 6 key bits below its cell's prefix);
+//  * a wave owns 64 curve-consecutive queries. A pass enumerates the level-lc cells
+//    around the wave's query box ARITHMETICALLY (cell coordinates from the quantised box
+//    ± the current radius; no pointer chasing), NEAREST FIRST: the cells' gaps to the box
+//    sit in the lanes and each round takes the smallest one still within the (shrinking)
+//    radius, so the bounds tighten before farther cells are reached;
+//  * per cell, one 16-byte vector load gives each lane one grandchild slot (prefetched one
+//    cell ahead) and one VALU pass tests all 64 against the box; runs of needed (or empty)
+//    slots are contiguous in memory and become one segment each;
+//  * a cell's segments are one candidate stream read with SCALAR loads (wave-uniform
+//    addresses through the constant address space): the candidates arrive in SGPRs and
+//    every VALU op of the canonical d² takes them as an operand — 6 VALU per candidate and
+//    lane, no broadcast, no per-row queues or logs; the next batch's loads (across segment
+//    boundaries) are issued before the current batch is computed.
 //
 // Every cull is conservative: cell boxes are the quantisation intervals widened by a
 // few ulps of the cube, the radius is inflated by 2^-16 (relative) over the largest lane
 // bound, so a skipped point always has canonical d² >= every lane's bound.
+//
+// Measured on one MI355X, uniform points, k = 100, this pass vs the bucket-tree kernel on
+// the same index (scripts/grid_ab.py, bit-identical outputs): 1e8 0.108 vs 0.124 s (with
+// sub-cells, before the 64-slot cells), 1B 1.20 vs 1.29 s; GRID=auto keeps clustered,
+// planar, duplicate and mixed-scale data on knn_rows (knn_engine.grid_applies).
 #include "dev.h"
 
 namespace {
@@ -227,8 +233,7 @@ __device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
 struct GridCtx {
   const float *pts;        // sorted points (packed float3, padded)
   const float *inf4;       // 4 x +inf (tail padding of a candidate batch)
-  const uint32_t *cells;   // level-lc (start, end) pairs, Morton index
-  const uint32_t *subs;    // level-lc+1 pairs
+  const uint4 *slots;      // [8^lc][64] grandchild runs (start, end, coords, -) in Hilbert order
   float ox, oy, oz;        // cube origin
   float scale;             // 1024 / extent (the sort keys' quantisation)
   float step;              // extent / 1024: one level-10 quantum
@@ -372,6 +377,108 @@ __device__ __forceinline__ void eval4(Lane &s, GridCtx &G, const Batch &b) {
   update4<MODE>(s, u0, u1, u2, u3, G.pool, G.lane);
 }
 
+// The 64 grandchild slots of one level-lc cell, fetched ahead of use (one 16-byte vector
+// load per lane: its counter retires in order, so the wait lands at the first use, one
+// cell later): lane j holds the j-th grandchild (level lc+2) IN HILBERT ORDER — the
+// order of the sorted array — as (start, end, packed coordinates); empty: (0, 0).
+struct CellLoad {
+  uint32_t a, e, xyz;  // per lane
+};
+__device__ __forceinline__ CellLoad fetch_cell(const GridCtx &G, uint32_t x, uint32_t y, uint32_t z) {
+  const uint32_t mc = lsk::morton3(x, y, z);
+  const uint4 v = G.slots[64u * mc + (uint32_t)G.lane];
+  return CellLoad{v.x, v.y, v.z};
+}
+
+template <int MODE>
+__device__ __forceinline__ void count_batch(GridCtx &G) {
+  G.evals += 4u;
+#ifdef LSK_GRID_PROFILE
+  G.ev_mode[MODE] += 4u;
+#endif
+}
+
+// The last batch of a segment: slots past its end count nowhere.
+template <int MODE>
+__device__ __forceinline__ void eval4_tail(Lane &s, GridCtx &G, const Batch &b, uint32_t left) {
+  const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
+  const uint32_t u1 = left > 1u ? fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1)) : ~0u;
+  const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
+  update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane);
+}
+
+// The candidates of one cell as ONE stream over its needed runs of grandchildren, 4 per
+// batch. Slots are in memory order, so a run of needed (or empty) slots is one
+// contiguous segment of the sorted array. The next batch's scalar loads — the next
+// segment's first batch at a segment end — are issued before the current batch is
+// computed, so short segments do not each pay a cold load latency. Unrolled by two with
+// A / B batch registers (a loop-carried copy would make the compiler wait for the prefetch
+// right after issuing it).
+//   need: needed non-empty slots; free: needed or empty slots (runs of `free` that hold
+//   a needed slot are the segments).
+template <int MODE>
+__device__ __forceinline__ void process_cell_stream(Lane &s, GridCtx &G, const CellLoad &c, uint64_t need,
+                                                    uint64_t free) {
+  const lsk::cfloat_p P = lsk::as_const(G.pts);
+  // pops the next segment: [start of its first needed slot, end of its last needed slot)
+  auto pop = [&](uint32_t &a, uint32_t &b) {
+    const uint32_t t0 = (uint32_t)__builtin_ctzll(need);
+    const uint64_t after = ~free >> t0;  // first slot past the run of free slots
+    const uint32_t len = after ? (uint32_t)__builtin_ctzll(after) : 64u - t0;
+    const uint64_t run = (len >= 64u ? ~0ull : ((1ull << len) - 1ull)) << t0;
+    const uint64_t in = need & run;
+    const uint32_t t1 = 63u - (uint32_t)__builtin_clzll(in);
+    need &= ~run;
+    a = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)c.a, (int)t0));
+    b = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)c.e, (int)t1));
+    G.segs++;
+  };
+  uint32_t i, e;
+  pop(i, e);
+  uint32_t chk = i + kSegCheck;
+  // position after batch i of [.., e): next batch of the segment, else the next segment
+  auto advance = [&](uint32_t &ni, uint32_t &ne) -> bool {
+    ni = i + 4u;
+    ne = e;
+    if (ni < e) return true;
+    if (!need) {
+      ni = i;  // (a dummy reload of the current batch: in flight, unused)
+      return false;
+    }
+    pop(ni, ne);
+    return true;
+  };
+  Batch A = load_batch(P, i);
+  for (;;) {
+    uint32_t ni, ne;
+    bool more = advance(ni, ne);
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    Batch B = load_batch(P, ni);
+    __builtin_amdgcn_sched_barrier(0);
+    if (e - i >= 4u) eval4<MODE>(s, G, A); else eval4_tail<MODE>(s, G, A, e - i);
+    count_batch<MODE>(G);
+    if (!more) break;
+    i = ni;
+    e = ne;
+    more = advance(ni, ne);
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    A = load_batch(P, ni);
+    __builtin_amdgcn_sched_barrier(0);
+    if (e - i >= 4u) eval4<MODE>(s, G, B); else eval4_tail<MODE>(s, G, B, e - i);
+    count_batch<MODE>(G);
+    if (!more) break;
+    i = ni;
+    e = ne;
+    if (MODE == MODE_HIST && i >= chk) {
+      // long stream (a crowded cell): once every lane's bound has closed (k exact copies:
+      // the k-th is 0) the rest of it cannot count
+      chk = i + kSegCheck;
+      shrink_all<MODE>(s, G);
+      if (!__ballot(s.state == ST_HIST && s.hi_b > 0u)) break;
+    }
+  }
+}
+
 // Unrolled by two with separate A / B batch registers: a loop-carried copy of the batch
 // would make the compiler wait for the prefetch right after issuing it.
 template <int MODE>
@@ -422,47 +529,19 @@ __device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0
 #endif
 }
 
-// Table entries of one level-lc cell, fetched ahead of use (vector loads: their counter
-// retires in order, so the wait lands at the first use, one cell later): lanes 0-7 hold
-// sub-cell j's (start, end), every other lane the cell's own.
-struct CellLoad {
-  uint32_t x, y, z;
-  uint32_t a, e;  // per lane
-};
-__device__ __forceinline__ CellLoad fetch_cell(const GridCtx &G, uint32_t x, uint32_t y, uint32_t z) {
-  const uint32_t mc = lsk::morton3(x, y, z);
-  const uint32_t *src = G.lane < 8 ? G.subs + 2u * (8u * mc + (uint32_t)G.lane) : G.cells + 2u * mc;
-  const uint2 v = *(const uint2 *)src;
-  return CellLoad{x, y, z, v.x, v.y};
-}
-
-// One level-lc cell: lanes 0-7 test its 8 sub-cells against the wave box; a fully needed
-// cell is one segment.
+// One level-lc cell: lane j tests grandchild j against the wave box.
 template <int MODE>
 __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad &c, float r2) {
-  const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)c.a, 8);
-  const uint32_t ce = (uint32_t)__builtin_amdgcn_readlane((int)c.e, 8);
-  if (cs >= ce) return;
+  const bool ne = c.e > c.a;
+  const uint64_t nonempty = __ballot(ne);
+  if (!nonempty) return;
   G.cells_n++;
-  const uint32_t j = (uint32_t)G.lane & 7u;
-  const uint32_t sh = 10u - (G.lc + 1u);
-  const float g2 = cell_gap2(G, 2u * c.x + ((j >> 2) & 1u), 2u * c.y + ((j >> 1) & 1u), 2u * c.z + (j & 1u), sh);
-  const bool sub = G.lane < 8 && c.e > c.a;
-  const uint32_t nonempty = (uint32_t)__ballot(sub);
-  const uint32_t need = (uint32_t)__ballot(sub && g2 <= r2);
-  if (need == 0u) return;
+  const uint32_t sh = 10u - (G.lc + 2u);
+  const float g2 = cell_gap2(G, c.xyz & 1023u, (c.xyz >> 10) & 1023u, c.xyz >> 20, sh);
+  const uint64_t need = __ballot(ne && g2 <= r2);
+  if (!need) return;
   LSK_GT(tp0);
-  if (need == nonempty) {
-    process_segment<MODE>(s, G, cs, ce);
-  } else {
-    uint32_t m = need;
-    while (m) {
-      const int b = __builtin_ctz(m);
-      m &= m - 1u;
-      process_segment<MODE>(s, G, (uint32_t)__builtin_amdgcn_readlane((int)c.a, b),
-                            (uint32_t)__builtin_amdgcn_readlane((int)c.e, b));
-    }
-  }
+  process_cell_stream<MODE>(s, G, c, need, need | ~nonempty);
   shrink_all<MODE>(s, G);
   LSK_GADD(G.prof[MODE], tp0);
 }
@@ -503,7 +582,7 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
     shrink_all<MODE>(s, G);
     return true;
   }
-  CellLoad pend{0u, 0u, 0u, 0u, 0u};
+  CellLoad pend{0u, 0u, 0u};
   bool have = false;
   const uint32_t nx = x1 - x0 + 1u, ny = y1 - y0 + 1u, nz = z1 - z0 + 1u;
   if (nx <= 16u && ny <= 16u && nx * ny * nz <= 256u) {
@@ -603,8 +682,7 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   GridCtx G;
   G.pts = A.tree[0].pts;
   G.inf4 = V.inf4;
-  G.cells = V.cells;
-  G.subs = V.subs;
+  G.slots = (const uint4 *)V.slots;
   {
     const lsk::cfloat_p bx = lsk::as_const(V.box);
     G.ox = bx[0];
@@ -654,7 +732,12 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
     const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
     if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
     const uint32_t mb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, max(1u, nvalid / 2u));
+#ifdef LSK_GRID_EST_MEDIAN
+    // one range for the whole wave (the cull radius follows the largest lane range)
+    if (ok && mb < lsk::kInfBits) r_est2 = bitsf(mb) * (float)LSK_GRID_EST_MEDIAN;
+#else
     if (ok && mb < lsk::kInfBits) r_est2 = sqrtf(r_est2 * bitsf(mb)) * kEstCalib;
+#endif
   }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
     r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
@@ -866,27 +949,33 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
 }
 
 // ------------------------------------------------------------------ grid build
-__device__ __forceinline__ uint32_t sub_morton(const float *p, float ox, float oy, float oz, float s, uint32_t sh) {
-  return lsk::morton3(lsk::morton_quant(p[0], ox, s) >> sh, lsk::morton_quant(p[1], oy, s) >> sh,
-                      lsk::morton_quant(p[2], oz, s) >> sh);
-}
-
-// Run boundaries of the level-(lc+1) sub-cells and level-lc cells along the sorted points.
-__global__ __launch_bounds__(256) void grid_build_kernel(const float *__restrict__ pts, int64_t n,
-                                                         const float *__restrict__ box, uint32_t ls,
-                                                         uint32_t *__restrict__ cells, uint32_t *__restrict__ subs) {
+// Runs of the level-g grandchildren (g = lc + 2) along the sorted points. A grandchild's
+// slot inside its level-lc cell is bits [6g-..] of its curve key: the 6 key bits below
+// the cell's prefix = its rank in curve order among the cell's 64 grandchildren, i.e. in
+// memory order (Hilbert and Morton keys alike: every aligned block of 8^l keys is one
+// octree cell). Slot = (start, end, x | y << 10 | z << 20 of the grandchild, 0).
+__global__ __launch_bounds__(256) void grid_build_kernel(const float *__restrict__ pts,
+                                                         const uint32_t *__restrict__ keys, int64_t n,
+                                                         const float *__restrict__ box, uint32_t g,
+                                                         uint4 *__restrict__ slots) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float ox = box[0], oy = box[1], oz = box[2], s = box[6];
-  const uint32_t sh = 10u - ls;
-  const uint32_t m = sub_morton(pts + 3 * i, ox, oy, oz, s, sh);
-  const uint32_t mp = i > 0 ? sub_morton(pts + 3 * (i - 1), ox, oy, oz, s, sh) : ~0u;
-  const uint32_t mn = i + 1 < n ? sub_morton(pts + 3 * (i + 1), ox, oy, oz, s, sh) : ~0u;
-  if (mp != m) subs[2u * m] = (uint32_t)i;
-  if (mn != m) subs[2u * m + 1u] = (uint32_t)(i + 1);
-  const uint32_t c = m >> 3;
-  if (i == 0 || (mp >> 3) != c) cells[2u * c] = (uint32_t)i;
-  if (i + 1 == n || (mn >> 3) != c) cells[2u * c + 1u] = (uint32_t)(i + 1);
+  const uint32_t ks = 3u * (10u - g);
+  const uint32_t kg = keys[i] >> ks;
+  const bool first = i == 0 || (keys[i - 1] >> ks) != kg;
+  const bool last = i + 1 == n || (keys[i + 1] >> ks) != kg;
+  if (!first && !last) return;
+  const float ox = box[0], oy = box[1], oz = box[2], sc = box[6];
+  const uint32_t sh = 10u - g;
+  const uint32_t x = lsk::morton_quant(pts[3 * i], ox, sc) >> sh;
+  const uint32_t y = lsk::morton_quant(pts[3 * i + 1], oy, sc) >> sh;
+  const uint32_t z = lsk::morton_quant(pts[3 * i + 2], oz, sc) >> sh;
+  uint32_t *slot = (uint32_t *)(slots + 64u * lsk::morton3(x >> 2, y >> 2, z >> 2) + (kg & 63u));
+  if (first) {
+    slot[0] = (uint32_t)i;
+    slot[2] = x | (y << 10) | (z << 20);
+  }
+  if (last) slot[1] = (uint32_t)(i + 1);
 }
 
 // counts[l] += number of i in [1, n) whose key prefix at level l (top 3l bits of the
@@ -919,15 +1008,16 @@ __global__ __launch_bounds__(256) void key_levels_kernel(const uint32_t *__restr
   }
 }
 
-// sum over sub-cells of (end - start)^2: the mean sub-cell population seen by a point is
-// this / n (uniform data: about the mean population + 1). Grid-stride, one atomic per block.
-__global__ __launch_bounds__(256) void grid_sq_kernel(const uint32_t *__restrict__ subs, int64_t nsub,
+// sum over grandchild slots of (end - start)^2: the mean grandchild population seen by a
+// point is this / n (uniform data: about the mean population + 1). Grid-stride, one
+// atomic per block.
+__global__ __launch_bounds__(256) void grid_sq_kernel(const uint4 *__restrict__ slots, int64_t nslot,
                                                       unsigned long long *__restrict__ out) {
   unsigned long long v = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsub; i += stride) {
-    const uint32_t a = subs[2 * i], b = subs[2 * i + 1];
-    const unsigned long long d = b > a ? (unsigned long long)(b - a) : 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslot; i += stride) {
+    const uint4 t = slots[i];
+    const unsigned long long d = t.y > t.x ? (unsigned long long)(t.y - t.x) : 0ull;
     v += d * d;
   }
 #pragma unroll
@@ -943,22 +1033,22 @@ __global__ __launch_bounds__(256) void grid_sq_kernel(const uint32_t *__restrict
 
 }  // namespace
 
-extern "C" int lsk_hip_grid_build(const float *sorted_pts, int64_t n, const float *box, int32_t level,
-                                  uint32_t *cells, uint32_t *subs, void *stream) {
-  if (level < 1 || level > 9) {
-    lsk::set_last_error("grid_build: level must be in [1, 9] (sub-cells at level + 1 <= 10)");
+extern "C" int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorted_keys, int64_t n,
+                                  const float *box, int32_t level, uint32_t *slots, void *stream) {
+  if (level < 0 || level > 8) {
+    lsk::set_last_error("grid_build: level must be in [0, 8] (grandchildren at level + 2 <= 10)");
     return 1;
   }
   if (n >= ((int64_t)1 << 32)) {
     lsk::set_last_error("grid_build: n must be < 2^32");
     return 1;
   }
-  const size_t ncell = (size_t)1 << (3 * level);
+  const size_t nslot = (size_t)64 << (3 * level);
   hipStream_t st = (hipStream_t)stream;
-  LSK_HIP(hipMemsetAsync(cells, 0, ncell * 8, st));
-  LSK_HIP(hipMemsetAsync(subs, 0, ncell * 64, st));
+  LSK_HIP(hipMemsetAsync(slots, 0, nslot * 16, st));
   if (n <= 0) return 0;
-  grid_build_kernel<<<lsk_blocks(n, 256), 256, 0, st>>>(sorted_pts, n, box, (uint32_t)level + 1u, cells, subs);
+  grid_build_kernel<<<lsk_blocks(n, 256), 256, 0, st>>>(sorted_pts, sorted_keys, n, box, (uint32_t)level + 2u,
+                                                        (uint4 *)slots);
   LSK_CHECK_LAUNCH("grid_build");
   return 0;
 }
@@ -972,11 +1062,11 @@ extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long
   return 0;
 }
 
-extern "C" int lsk_hip_grid_sq(const uint32_t *subs, int64_t nsub, unsigned long long *out, void *stream) {
+extern "C" int lsk_hip_grid_sq(const uint32_t *slots, int64_t nslot, unsigned long long *out, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   LSK_HIP(hipMemsetAsync(out, 0, sizeof(unsigned long long), st));
-  if (nsub <= 0) return 0;
-  grid_sq_kernel<<<lsk_blocks(nsub, 256, kLevelsBlocks), 256, 0, st>>>(subs, nsub, out);
+  if (nslot <= 0) return 0;
+  grid_sq_kernel<<<lsk_blocks(nslot, 256, kLevelsBlocks), 256, 0, st>>>((const uint4 *)slots, nslot, out);
   LSK_CHECK_LAUNCH("grid_sq");
   return 0;
 }
@@ -988,9 +1078,9 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
     return 1;
   }
   if (A.nq >= ((int64_t)1 << 32) || A.ntrees != 1 || A.groups || A.init_d2 ||
-      A.tree[0].n >= ((int64_t)1 << 32) || !grid || grid->level < 1 || grid->level > 9) {
+      A.tree[0].n >= ((int64_t)1 << 32) || !grid || grid->level < 0 || grid->level > 8) {
     lsk::set_last_error("knn_grid: one tree (< 2^32 points, the queries' own), no groups / init_d2, "
-                        "grid level in [1, 9]");
+                        "grid level in [0, 8]");
     return 1;
   }
   const int64_t ngroups = (A.nq + 63) / 64;

@@ -139,24 +139,26 @@ int lsk_hip_knn_exact(const lsk_knn_args *args, const uint32_t *list, const uint
                       int64_t cap, void *stream);
 
 // ---- cell-grid candidate source (knn_grid.hip) -----------------------------------------
-// Two octree levels over the Hilbert-sorted points of one tree (cube = the sort keys' box):
-// cells of level `level` and their sub-cells (level + 1 <= 10), each a contiguous run of
-// the sorted array stored as a (start, end) uint32 pair at its Morton index (empty: 0, 0).
+// Octree grid over the curve-sorted points of one tree (cube = the sort keys' box): every
+// cell of level `level` has 64 slots, one per grandchild (level + 2 <= 10) in curve order
+// (= memory order), each the grandchild's contiguous run of the sorted array:
+// (start, end, x | y << 10 | z << 20, 0) as uint32 x 4; empty: (0, 0, ...). Cells are
+// indexed by the Morton code of their coordinates.
 typedef struct lsk_grid_view {
-  const uint32_t *cells;  // [8^level][2]
-  const uint32_t *subs;   // [8^(level+1)][2]
+  const uint32_t *slots;  // [8^level * 64][4]
+  const uint32_t *pad_;   // (unused)
   const float *box;       // [8] device: the box of the sort keys (lo.xyz, hi.xyz, scale, extent)
-  const float *inf4;      // [4] device: +inf (candidate padding)
+  const float *inf4;      // [4] device: +inf (unused padding source)
   int32_t level;
   int32_t pad;
 } lsk_grid_view;
-int lsk_hip_grid_build(const float *sorted_pts, int64_t n, const float *box, int32_t level, uint32_t *cells,
-                       uint32_t *subs, void *stream);
+int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorted_keys, int64_t n, const float *box,
+                       int32_t level, uint32_t *slots, void *stream);
 // counts[l] (l = 1..10, 11 slots, zeroed here) = number of adjacent sorted keys whose level-l
 // prefixes differ (distinct level-l cells = counts[l] + 1).
 int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream);
-// out[0] = sum over sub-cells of population^2 (zeroed here).
-int lsk_hip_grid_sq(const uint32_t *subs, int64_t nsub, unsigned long long *out, void *stream);
+// out[0] = sum over slots of population^2 (zeroed here).
+int lsk_hip_grid_sq(const uint32_t *slots, int64_t nslot, unsigned long long *out, void *stream);
 // Near-uniform fast path of lsk_hip_knn_rows (same contract, same failure list): one tree
 // whose points are the queries, no groups / init_d2; candidates from the grid.
 int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *stream);

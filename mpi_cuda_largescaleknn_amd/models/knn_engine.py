@@ -64,23 +64,23 @@ class KnnConfig:
 # GPU indexes whose sub-cell populations look near-uniform (GRID_CROWD), "on" = always,
 # "off" = never (the bucket-tree kernel knn_rows serves every query).
 GRID = os.environ.get("LSKNN_GRID", "auto")
-GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "32"))  # target mean points per sub-cell
+GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "6"))  # target mean points per finest cell
 # auto: a point's sub-cell holds on average at most this many times the mean (+1)
 GRID_CROWD = float(os.environ.get("LSKNN_GRID_CROWD", "2"))
 
 
 @dataclass
 class GridIndex:
-    cells: torch.Tensor      # int32 [8^level, 2] (start, end) of each level-`level` cell
-    subs: torch.Tensor       # int32 [8^(level+1), 2] of each sub-cell
-    level: int
+    slots: torch.Tensor      # int32 [8^level * 64, 4]: per level-`level` cell, its 64
+                             # grandchildren's runs of the sorted array in curve order
+    level: int               # cell level (grandchildren at level + 2)
     box: torch.Tensor        # the cube of the sort keys (device)
     inf4: torch.Tensor | None = None  # 4 x +inf on the device (candidate padding)
 
     def view(self) -> tuple:
         if self.inf4 is None:
-            self.inf4 = torch.full((4,), math.inf, dtype=torch.float32, device=self.cells.device)
-        return (self.cells, self.subs, self.level, self.box, self.inf4)
+            self.inf4 = torch.full((4,), math.inf, dtype=torch.float32, device=self.slots.device)
+        return (self.slots, self.level, self.box, self.inf4)
 
 
 @dataclass
@@ -145,11 +145,12 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
 
 
 def grid_level(distinct: list[int], n: int, ms: float = GRID_MS) -> int:
-    """Sub-cell level of the grid: the level whose occupied sub-cells hold closest to `ms`
-    points on average, in log scale (uniform points in a cube, ms = 32: 1B -> 8 (60 per
-    sub-cell), 1e8 -> 7 (48), 2e7 -> 6 (76), 1e7 -> 6 (38)), in [2, 10]. Measured best on
-    uniform data, k = 100 and 16 (scripts/grid_ab.py): coarse sub-cells cost more
-    candidates, fine ones more cells and segments."""
+    """Level of the grid's finest cells (the grandchildren whose runs the k-NN pass
+    streams; enumerated through their level-2 ancestors): the level whose occupied cells
+    hold closest to `ms` points on average, in log scale (uniform points in a cube, ms = 6:
+    1B -> 9 (7.5 per cell), 1e8 -> 8 (6.0), 1e7 -> 7 (4.8)), in [2, 10]. Finer levels cull
+    more candidates (at 1e8, k=100: level 8 3.6K evaluations per query vs 4.6K at 7), and
+    merged runs keep the segments long."""
     best, err = 2, math.inf
     for lvl in range(2, 11):
         if distinct[lvl] <= 0:
@@ -160,12 +161,12 @@ def grid_level(distinct: list[int], n: int, ms: float = GRID_MS) -> int:
     return best
 
 
-def grid_applies(distinct: list[int], n: int, ls: int) -> bool:
+def grid_applies(distinct: list[int], n: int, g: int) -> bool:
     """GRID=auto: near-uniform 3-D data at the grid's scale — occupied cells multiply by
-    >= 6 from level ls-1 to ls (planar data: 4, exact copies: 1), and the level's mean
-    population is within [4, 256] points."""
-    mean = n / max(1, distinct[ls])
-    return distinct[ls] >= 6 * distinct[ls - 1] and 4.0 <= mean <= 256.0
+    >= 6 from level g-1 to g (planar data: 4, exact copies: 1), and the level's mean
+    population is within [2, 256] points."""
+    mean = n / max(1, distinct[g])
+    return distinct[g] >= 6 * distinct[g - 1] and 2.0 <= mean <= 256.0
 
 
 def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
@@ -177,16 +178,16 @@ def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
     if GRID == "off" or n == 0 or not K.is_gpu(index.pts) or torch.cuda.is_current_stream_capturing():
         return None
     distinct = K.key_levels(skeys[:n])
-    ls = grid_level(distinct, n)
-    if GRID == "auto" and not grid_applies(distinct, n, ls):
+    g = grid_level(distinct, n)
+    if GRID == "auto" and not grid_applies(distinct, n, g):
         return None
-    cells, subs = K.grid_build(index.pts, n, index.box, ls - 1)
+    slots = K.grid_build(index.pts, skeys, n, index.box, g - 2)
     if GRID == "auto":
-        seen = K.grid_sq(subs) / n          # mean population of a point's own sub-cell
-        mean = n / max(1, distinct[ls])
+        seen = K.grid_sq(slots) / n          # mean population of a point's own grandchild
+        mean = n / max(1, distinct[g])
         if seen > GRID_CROWD * (mean + 1.0):
             return None
-    return GridIndex(cells, subs, ls - 1, index.box)
+    return GridIndex(slots, g - 2, index.box)
 
 
 HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key

@@ -283,7 +283,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     out_perm / out_final (optional, fused scatter): the kernels also write
     out_final[out_perm[q]] = final distance; out_d2 may then be None.
     debug_fail_mod (tests): the rows kernel also fails every query q with q % mod == 0.
-    grid (impl "grid"): (cells, subs, level, box) of knn_engine.GridIndex — the cell-grid
+    grid (impl "grid"): (slots, level, box, inf4) of knn_engine.GridIndex — the cell-grid
     candidate source of knn_grid.hip for one tree whose points are the queries (same
     failure list and backstop as "rows").
     Returns the launch's FailWord.
@@ -335,8 +335,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_count = _ptr(count)
     a.fail_cap = cap
     if impl == "grid":
-        cells, subs, level, gbox, inf4 = grid
-        gv = GridView(_ptr(cells), _ptr(subs), _ptr(gbox), _ptr(inf4), int(level), 0)
+        slots, level, gbox, inf4 = grid
+        gv = GridView(_ptr(slots), None, _ptr(gbox), _ptr(inf4), int(level), 0)
         check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
     else:
         check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
@@ -358,21 +358,21 @@ def key_levels(skeys: torch.Tensor) -> list[int]:
     return [1] + [int(c[l]) + 1 for l in range(1, 11)]
 
 
-def grid_build(sorted_pts: torch.Tensor, n: int, box: torch.Tensor, level: int):
-    """(start, end) runs of the level-`level` cells and their level+1 sub-cells along the
-    sorted points (knn_grid.hip) -> (cells [8^level, 2], subs [8^(level+1), 2]) int32."""
+def grid_build(sorted_pts: torch.Tensor, sorted_keys: torch.Tensor, n: int, box: torch.Tensor, level: int):
+    """Grandchild runs of the octree grid over the curve-sorted points (knn_grid.hip): every
+    level-`level` cell has 64 slots (its level+2 grandchildren in curve order), each
+    (start, end, packed coords, 0) -> int32 [8^level * 64, 4]."""
     dev = sorted_pts.device
-    cells = torch.empty((1 << (3 * level), 2), dtype=torch.int32, device=dev)
-    subs = torch.empty((1 << (3 * level + 3), 2), dtype=torch.int32, device=dev)
-    check(_native.hip().lsk_hip_grid_build(_ptr(sorted_pts), n, _ptr(box), level, _ptr(cells), _ptr(subs),
+    slots = torch.empty((64 << (3 * level), 4), dtype=torch.int32, device=dev)
+    check(_native.hip().lsk_hip_grid_build(_ptr(sorted_pts), _ptr(sorted_keys), n, _ptr(box), level, _ptr(slots),
                                            _stream(sorted_pts)), "grid_build")
-    return cells, subs
+    return slots
 
 
-def grid_sq(subs: torch.Tensor) -> int:
-    """Sum over sub-cells of population^2 (host read)."""
-    out = torch.empty(1, dtype=torch.int64, device=subs.device)
-    check(_native.hip().lsk_hip_grid_sq(_ptr(subs), subs.shape[0], _ptr(out), _stream(subs)), "grid_sq")
+def grid_sq(slots: torch.Tensor) -> int:
+    """Sum over grid slots of population^2 (host read)."""
+    out = torch.empty(1, dtype=torch.int64, device=slots.device)
+    check(_native.hip().lsk_hip_grid_sq(_ptr(slots), slots.shape[0], _ptr(out), _stream(slots)), "grid_sq")
     return int(out.item())
 
 

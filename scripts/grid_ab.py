@@ -28,15 +28,15 @@ t = time.perf_counter()
 E.GRID = "on"
 idx = E.build_index(p, grid=True)
 torch.cuda.synchronize()
-print(f"build (tree + grid level {idx.grid.level}): {time.perf_counter() - t:.3f} s", flush=True)
+print(f"build (tree + grid, finest level {idx.grid.level + 2}): {time.perf_counter() - t:.3f} s", flush=True)
 cfg = E.KnnConfig(k=a.k)
 hint2 = E.radius_hint2(idx.box, n, a.k)
 grids = {"grid": idx.grid}
 if a.levels:
     from mpi_cuda_largescaleknn_amd.ops import kernels as K  # noqa: E402
-    for ls in [int(x) for x in a.levels.split(",")]:
-        c, s_ = K.grid_build(idx.pts, n, idx.box, ls - 1)
-        grids[f"grid-L{ls}"] = E.GridIndex(c, s_, ls - 1, idx.box)
+    skeys, _ = K.morton(idx.pts[:n], idx.box, with_iota=False)  # keys of the sorted points
+    for g in [int(x) for x in a.levels.split(",")]:  # finest level (cells at g - 2)
+        grids[f"grid-L{g}"] = E.GridIndex(K.grid_build(idx.pts, skeys, n, idx.box, g - 2), g - 2, idx.box)
 res = {}
 for impl in list(grids) + ["rows"]:
     idx.grid = grids.get(impl)

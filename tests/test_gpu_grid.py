@@ -32,26 +32,32 @@ def grid_knn(p, k, max_radius=math.inf, mode="on"):
 
 
 @pytest.mark.parametrize("n", [1, 100, 5000, 200_003])
-def test_grid_tables_match_torch(n):
+def test_grid_slots_match_torch(n):
+    """Every level-`lc` cell's 64 slots hold its grandchildren's runs of the sorted array
+    in curve order: (start, end, packed coordinates) — checked against a torch rebuild."""
     p = uniform(n, seed=n).to(DEV)
     idx = E.build_index(p)
-    for level in (1, 3, 5):
-        cells, subs = K.grid_build(idx.pts, n, idx.box, level)
-        box = idx.box.cpu()
-        q = ((idx.pts[:n].cpu() - box[0:3]) * box[6]).clamp(0, 1023).to(torch.int64)
-        for lv, tab in ((level, cells), (level + 1, subs)):
-            c = q >> (10 - lv)
-            m = torch.zeros(n, dtype=torch.int64)
-            for b in range(lv):  # Morton index: x bit 2, y bit 1, z bit 0 of each triple
-                for a, sh in ((0, 2), (1, 1), (2, 0)):
-                    m |= ((c[:, a] >> b) & 1) << (3 * b + sh)
-            assert bool((m[1:] != m[:-1]).sum() + 1 == torch.unique(m).numel())  # runs contiguous
-            ref = torch.zeros((1 << (3 * lv), 2), dtype=torch.int64)
-            uniq, first = torch.unique_consecutive(m, return_counts=True)
-            starts = torch.cumsum(first, 0) - first
-            ref[uniq, 0] = starts
-            ref[uniq, 1] = starts + first
-            assert torch.equal(tab.cpu().to(torch.int64), ref)
+    box = idx.box.cpu()
+    keys, _ = K.morton(idx.pts[:n].cpu(), box)  # curve keys of the sorted points
+    for lc in (0, 2, 4):
+        g = lc + 2
+        slots = K.grid_build(idx.pts, keys.to(DEV), n, idx.box, lc).cpu().to(torch.int64)
+        q = ((idx.pts[:n].cpu() - box[0:3]) * box[6]).clamp(0, 1023).to(torch.int64) >> (10 - g)
+        kg = (keys.to(torch.int64) & 0x3FFFFFFF) >> (3 * (10 - g))
+        assert bool((kg[1:] >= kg[:-1]).all())  # sorted by the grandchild prefix
+        cm = torch.zeros(n, dtype=torch.int64)
+        c = q >> 2
+        for b in range(lc):  # Morton index of the level-lc cell: x bit 2, y bit 1, z bit 0
+            for a, sh in ((0, 2), (1, 1), (2, 0)):
+                cm |= ((c[:, a] >> b) & 1) << (3 * b + sh)
+        ref = torch.zeros((64 << (3 * lc), 4), dtype=torch.int64)
+        uniq, cnt = torch.unique_consecutive(kg, return_counts=True)
+        starts = torch.cumsum(cnt, 0) - cnt
+        row = cm[starts] * 64 + (uniq & 63)
+        ref[row, 0] = starts
+        ref[row, 1] = starts + cnt
+        ref[row, 2] = q[starts, 0] | (q[starts, 1] << 10) | (q[starts, 2] << 20)
+        assert torch.equal(slots[:, :3], ref[:, :3]), lc
 
 
 @pytest.mark.parametrize("dist", list(GENERATORS))
