@@ -383,15 +383,17 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
                    grid=index.grid.view() if use_grid else None, **kw)
-    def check():
+    def check() -> bool:
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun
-        # the whole query on the exact kernel
+        # the whole query on the exact kernel (on the current stream; returns True then)
         nfail = fw.value()
-        if nfail > fw.cap:
+        rerun = nfail > fw.cap
+        if rerun:
             K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", **kw)
         if stats is not None:
             stats.add_fallback(nfail)
             stats.add(raw)
+        return rerun
 
     if torch.cuda.is_current_stream_capturing():
         slot = len(CAPTURED_FAIL_WORDS)
@@ -405,16 +407,21 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
         if stats is not None:
             stats.add(raw)
     elif deferred is not None:
+        fw.stage()  # the later read waits for this launch only
         deferred.append(check)
     else:
         check()
     return out if want_d2 else final_out
 
 
-def settle(deferred: list) -> None:
-    """Run the failure checks `query(..., deferred=...)` queued (in launch order)."""
+def settle(deferred: list) -> bool:
+    """Run the failure checks `query(..., deferred=...)` queued (in launch order). True
+    when one of them queued a rerun (its output is rewritten behind the current stream's
+    work: a copy of it queued earlier is stale)."""
+    rerun = False
     while deferred:
-        deferred.pop(0)()
+        rerun = bool(deferred.pop(0)()) or rerun
+    return rerun
 
 
 def verify_captured_failures(clear: bool = False) -> int:

@@ -254,10 +254,28 @@ class FailWord:
     def __init__(self, count: torch.Tensor | None, cap: int):
         self.count = count
         self.cap = cap
+        self._host = None
+        self._ev = None
+
+    def stage(self) -> None:
+        """Queue the word's copy to pinned host memory on the current stream (right behind
+        the launch): a later value() waits for this launch only, not for work queued on
+        the stream after it."""
+        if self.count is None or self.count.device.type != "cuda":
+            return
+        self._host = torch.empty(1, dtype=self.count.dtype, pin_memory=True)
+        self._host.copy_(self.count, non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
 
     def value(self) -> int:
         # the kernels count in uint32 (a count >= 2^31 must not read as negative)
-        return 0 if self.count is None else int(self.count.item()) & 0xFFFFFFFF
+        if self.count is None:
+            return 0
+        if self._ev is not None:
+            self._ev.synchronize()
+            return int(self._host[0]) & 0xFFFFFFFF
+        return int(self.count.item()) & 0xFFFFFFFF
 
     def overflowed(self) -> bool:
         return self.value() > self.cap

@@ -764,6 +764,8 @@ class Redistributed:
     recv_counts: list
     send_perm: torch.Tensor      # local input row of each sent row
     send_counts: list
+    index: E.LocalIndex | None = None  # built ahead (SetStream), else by compute_set
+    index_ready: object = None         # event after which `index` is complete
 
 
 def redistribute_set(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
@@ -782,15 +784,36 @@ def redistribute_set(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total
     return Redistributed(int(points.shape[0]), box, hint2, owned, recv_counts, send_perm, send_counts)
 
 
+def build_ahead(P: Redistributed, stream, users) -> None:
+    """Build P's index on `stream` (after the work queued there so far) and mark it ready
+    with an event; its tensors are kept for the streams in `users` (record_stream)."""
+    with torch.cuda.stream(stream):
+        index = E.build_index(P.owned, P.box, grid=True)
+    P.owned.record_stream(stream)
+    for t in (index.pts, index.perm, index.nodes, index.qnodes, index.box) + \
+            ((index.grid.slots,) if index.grid is not None else ()):
+        for u in users:
+            t.record_stream(u)
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    P.index, P.index_ready = index, ev
+
+
 def compute_set(P: Redistributed, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
                 out: torch.Tensor | None = None, hook=None) -> torch.Tensor:
-    """Second half: bucket tree of the owned points, local k-NN + halo exchange + re-query,
+    """Second half: bucket tree of the owned points (or P.index built ahead), local k-NN +
+    halo exchange + re-query,
     distances back to their origin ranks in input order (into `out` if given). `hook`:
     see knn_with_halo; it returns the stream its collectives ran on, and the result
     return is ordered after it (one communicator: no concurrent collectives)."""
     info = info or RunInfo(PhaseTimer(False, comm.device))
     dev = comm.device
-    index = E.build_index(P.owned, P.box, grid=True)
+    if P.index is not None:
+        index = P.index
+        if P.index_ready is not None:
+            torch.cuda.current_stream(dev).wait_event(P.index_ready)
+    else:
+        index = E.build_index(P.owned, P.box, grid=True)
     info.timer.mark("build")
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     used: list = []

@@ -27,6 +27,7 @@ Measured on one MI355X (1B uniform, k=100, two alternating sets): 1414 ms per se
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Sequence
 
 import torch
@@ -37,6 +38,18 @@ from . import pipelines as PL
 from .comm import Comm
 
 
+# one rank: set i+1's index is built on the high-priority side stream under set i's k-NN
+# (measured slower: 1B k=100 1168 vs 1106 ms per set; the build's workgroups hold CU slots
+# among the k-NN's far longer than the build takes alone — kept as an option)
+BUILD_AHEAD = os.environ.get("LSKNN_BUILD_AHEAD", "0") != "0"
+
+
+def _index_tensors(index: E.LocalIndex):
+    yield from (index.pts, index.perm, index.nodes, index.qnodes, index.box)
+    if index.grid is not None:
+        yield index.grid.slots
+
+
 class SetStream:
     """Runs `unordered_knn` over a sequence of host point sets with the transfers of
     neighbouring sets overlapped (see module doc).
@@ -45,12 +58,16 @@ class SetStream:
     the distances into the pinned host outputs itself (pipelines.direct_host_out_pays).
     """
 
-    def __init__(self, comm: Comm, cfg: E.KnnConfig, direct_out: bool = True):
+    def __init__(self, comm: Comm, cfg: E.KnnConfig, direct_out: bool = True,
+                 build_ahead: bool | None = None):
         self.comm = comm
         self.cfg = cfg
         self.device = comm.device
         self.gpu = self.device.type == "cuda"
         self.direct_out = bool(direct_out) and not comm.distributed
+        if build_ahead is None:
+            build_ahead = BUILD_AHEAD
+        self.build_ahead = bool(build_ahead)
         if self.gpu:
             self.copy_stream = torch.cuda.Stream(self.device)
             self.out_stream = torch.cuda.Stream(self.device)
@@ -103,14 +120,16 @@ class SetStream:
             return
         if self.comm.distributed:
             return self._run_distributed(inputs, outputs, n_totals, new_info, done)
+        if self.build_ahead:  # (one rank)
+            return self._run_build_ahead(inputs, outputs, n_totals, new_info, done)
         cur = torch.cuda.current_stream(self.device)
         if n:
             self._prefetch(0, inputs[0])
         # no host sync between sets: set i+1's build is queued right behind set i's k-NN
-        # (the stream orders them), and set i's failure-word read (a host sync, see
-        # knn_engine.query `deferred`) waits until set i+1's work is queued
-        pend: list = []
-        fin: list = []  # (set, event after which its output is in host memory)
+        # (the stream orders them), and set i's failure-word read (a host sync on an event
+        # right behind its k-NN, see knn_engine.query `deferred`) comes once set i+1's work
+        # is queued; set i's output copy follows that check (a rerun rewrites the output)
+        prev = None  # set i-1: see _query
         for i in range(n):
             cur.wait_stream(self.copy_stream)  # set i's points are on the device
             pts = self._dbuf[i % 2]
@@ -120,37 +139,126 @@ class SetStream:
             with trace.range(f"lsknn:set {i}"):
                 info.timer.start()
                 index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info)
-                E.settle(pend)  # set i-1's failure word: its k-NN ran before this build
-                direct = self.direct_out
-                res = PL.local_query(index, hint2, self.cfg, info, outputs[i] if direct else None,
-                                     deferred=pend)
-                ev = torch.cuda.Event()
-                if res.data_ptr() != outputs[i].data_ptr():
-                    # device results: their copy to host runs on a side stream under the
-                    # next set's build and k-NN
-                    self.out_stream.wait_stream(cur)
-                    with torch.cuda.stream(self.out_stream):
-                        outputs[i].copy_(res, non_blocking=True)
-                        ev.record(self.out_stream)
-                    res.record_stream(self.out_stream)
-                else:
-                    ev.record(cur)
-                del res, index
+                rel = self._release(prev, outputs) if prev is not None else None
+                rec = self._query(i, index, hint2, info, outputs)
+                del index
+            if rel is not None:  # set i-1's output, waited for once set i's k-NN is queued
+                rel[1].synchronize()
+                done(rel[0])
             self.last_info = info
-            fin.append((i, ev))
-            while len(fin) > 1:  # set i-1 (queued before set i's work) is retired
-                j, e = fin.pop(0)
-                e.synchronize()
-                done(j)
-        E.settle(pend)
-        torch.cuda.synchronize(self.device)  # the last results are in host memory
-        for j, _ in fin:
-            done(j)
+            prev = rec
+        if prev is not None:
+            self._retire(prev, outputs, done)
+
+    def _query(self, i, index, hint2, info, outputs):
+        """Queue set i's k-NN (the kernel writes the pinned output itself when direct);
+        returns (i, device result or None, event after the k-NN, its deferred failure
+        checks)."""
+        cur = torch.cuda.current_stream(self.device)
+        pend: list = []
+        res = PL.local_query(index, hint2, self.cfg, info, outputs[i] if self.direct_out else None,
+                             deferred=pend)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        return (i, None if res.data_ptr() == outputs[i].data_ptr() else res, ev, pend)
+
+    def _retire(self, rec, outputs, done) -> None:
+        j, ev = self._release(rec, outputs)
+        ev.synchronize()
+        done(j)
+
+    def _release(self, rec, outputs):
+        """Set j: its failure check (a 4-byte read behind its k-NN), then its device result
+        to host on the output stream (behind its k-NN, or behind everything queued so far
+        when the check queued a rerun). Returns (j, event after which outputs[j] is in
+        host memory)."""
+        j, res, ev, pend = rec
+        cur = torch.cuda.current_stream(self.device)
+        if E.settle(pend):
+            ev = torch.cuda.Event()
+            ev.record(cur)
+        if res is not None:
+            self.out_stream.wait_event(ev)
+            with torch.cuda.stream(self.out_stream):
+                outputs[j].copy_(res, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.out_stream)
+            res.record_stream(self.out_stream)
+        return j, ev
+
+    def _run_build_ahead(self, inputs, outputs, n_totals, new_info, done) -> None:
+        """One rank, index builds off the compute stream: set i+1's bounds, sort, tree and
+        grid are queued on the high-priority side stream right after set i's k-NN launch.
+        The k-NN grid is VALU-bound and the build kernels memory-bound; the build's
+        workgroups take CU slots as the k-NN's retire, so the compute stream runs k-NN after
+        k-NN with no build between them. The index tensors are allocated on the side stream
+        and read on the compute stream (record_stream keeps them until that read is done).
+        Sets alive at once: the one being retired, the one in the k-NN, the one being built
+        and the one being uploaded after the retired one is released."""
+        n = len(inputs)
+        dev = self.device
+        cur = torch.cuda.current_stream(dev)
+        side = self.redist_stream
+        if n == 0:
+            return
+
+        def build(j: int):
+            # set j's points are on the device (copy stream), then its index on `side`
+            side.wait_stream(self.copy_stream)
+            info = new_info()
+            info.timer.start()
+            with torch.cuda.stream(side):
+                pts = self._dbuf[j % 2]
+                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[j] or pts.shape[0], info)
+            for t in _index_tensors(index):
+                t.record_stream(cur)
+            if isinstance(hint2, torch.Tensor):
+                hint2.record_stream(cur)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            return index, hint2, info, ev
+
+        self._prefetch(0, inputs[0])
+        nxt = build(0)
+        if n > 1:
+            self._prefetch_after(1, inputs[1], None)
+        prev = None
+        for i in range(n):
+            index, hint2, info, bev = nxt
+            cur.wait_event(bev)
+            with trace.range(f"lsknn:set {i}"):
+                rec = self._query(i, index, hint2, info, outputs)
+            del index
+            if i + 1 < n:
+                nxt = build(i + 1)  # under set i's k-NN
+            if prev is not None:
+                # set i-1's failure word (its k-NN ran before set i's; a rerun goes behind
+                # set i's k-NN with set i-1's index still alive), output, release
+                self._retire(prev, outputs, done)
+            if i + 2 < n:
+                # set i+2 reuses set i's input buffer: free once set i's build is done
+                self._prefetch_after(i + 2, inputs[i + 2], bev)
+            self.last_info = info
+            prev = rec
+        self._retire(prev, outputs, done)
+
+    def _build_stream(self):
+        if getattr(self, "_bst", None) is None:
+            self._bst = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
+        return self._bst
+
+    def _prefetch_after(self, j: int, host: torch.Tensor, ev) -> None:
+        # copy set j into its buffer once `ev` (the build that last read it) is done
+        if ev is not None:
+            self.copy_stream.wait_event(ev)
+        with torch.cuda.stream(self.copy_stream):
+            self._buffer(j % 2, host).copy_(host, non_blocking=True)
 
     def _run_distributed(self, inputs, outputs, n_totals, new_info, done) -> None:
         comm, cfg, dev = self.comm, self.cfg, self.device
         cur = torch.cuda.current_stream(dev)
         redist = self.redist_stream
+        bst = self._build_stream()
         n = len(inputs)
         for j in range(n):  # global point counts (one small all-reduce per unknown set)
             if n_totals[j] is None:
@@ -176,6 +284,11 @@ class SetStream:
                 redist.wait_stream(self.copy_stream)
                 with torch.cuda.stream(redist):
                     nxt["P"] = PL.redistribute_set(self._dbuf[j % 2], comm, cfg, n_totals[j])
+                if self.build_ahead:
+                    # and its index, on a stream of its own (the collectives' stream, which
+                    # set i's halo exchange and result return wait for, stays short)
+                    bst.wait_stream(redist)
+                    PL.build_ahead(nxt["P"], bst, [cur])
                 return redist
 
             with trace.range(f"lsknn:set {i}"):

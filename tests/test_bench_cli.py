@@ -76,12 +76,15 @@ def test_bench_single_gpu_pipelined():
 
 
 @pytest.mark.gpu
-def test_bench_pipelined_forced_rccl_single_gpu():
+@pytest.mark.parametrize("ahead", ["1", "0"])
+def test_bench_pipelined_forced_rccl_single_gpu(ahead):
     """--pipeline 1 on the multi-rank path (1-rank RCCL group): device-resident input per
-    step, plain (non-streamed) redistribution, both sets exact."""
+    step, plain (non-streamed) redistribution, the next set's index built ahead on a side
+    stream (or by compute_set), both sets exact."""
     out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
                           "--force-dist", "--pipeline", "1"],
-                         cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port())),
+                         cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                                            LSKNN_BUILD_AHEAD=ahead),
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = _json_line(out.stdout)

@@ -53,16 +53,19 @@ def test_stream_length_mismatch():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("direct", [True, False])
-def test_stream_single_gpu(direct):
+@pytest.mark.parametrize("ahead", [True, False])
+def test_stream_single_gpu(direct, ahead):
     """One rank on the GPU: pinned host sets of different sizes, the kernel writing the
-    pinned outputs directly (or device results copied back), equal to the CPU oracle."""
+    pinned outputs directly (or device results copied back), the next set's index built
+    on the side stream under the current k-NN (or on the compute stream between them),
+    equal to the CPU oracle."""
     k = 16
     cfg = E.KnnConfig(k=k)
     dev = torch.device("cuda", torch.cuda.current_device())
-    S = sets()
+    S = sets() + [GENERATORS["uniform"](30_000, seed=5)]
     ins = [p.pin_memory() for p in S]
     outs = [torch.full((p.shape[0],), -1.0).pin_memory() for p in S]
-    runner = SetStream(SingleComm(dev), cfg, direct_out=direct)
+    runner = SetStream(SingleComm(dev), cfg, direct_out=direct, build_ahead=ahead)
     runner.run(ins, outs)
     for i, p in enumerate(S):
         assert torch.equal(outs[i], oracle(p, k)), i
