@@ -49,7 +49,18 @@ using lsk::fbits;
 constexpr int kWPB = LSK_GRID_WPB;
 constexpr int kThreads = kWPB * lsk::kWave;
 constexpr int kBins = 40;                 // 16-bit bins, two per LDS dword (as knn_rows)
+// LSK_GRID_PAIRHIST: lanes l and l+32 share a dword (low / high half) of each bin row, so
+// a lane's increment is a per-lane constant and every candidate adds without a branch
+// (values past the range go to a trash row, kBins); else (as knn_rows) bins 2j and 2j+1
+// of one lane share a dword.
+#ifndef LSK_GRID_PAIRHIST
+#define LSK_GRID_PAIRHIST 0
+#endif
+#if LSK_GRID_PAIRHIST
+constexpr int kPool = (kBins + 1) * 32;   // dwords per wave: histogram + trash row, or collect pool
+#else
 constexpr int kPool = kBins / 2 * 64;     // dwords per wave: histogram, or collect pool
+#endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -109,7 +120,11 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
 }
 
 __device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
+#if LSK_GRID_PAIRHIST
+  return (pool[b * 32u + ((uint32_t)lane & 31u)] >> (((uint32_t)lane & 32u) >> 1)) & 0xffffu;
+#else
   return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
+#endif
 }
 
 __device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *pool, int lane) {
@@ -145,11 +160,16 @@ __device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int l
 // equals c_hi iff no counter wrapped.
 __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *pool, int lane) {
   uint32_t sum = 0;
+#if LSK_GRID_PAIRHIST
+#pragma unroll
+  for (int b = 0; b < kBins; b++) sum += b < s.bin_hi ? hist_read(pool, (uint32_t)b, lane) : 0u;
+#else
 #pragma unroll
   for (int j = 0; j < kBins / 2; j++) {
     const uint32_t w = pool[j * lsk::kWave + lane];
     sum += (2 * j < s.bin_hi ? (w & 0xffffu) : 0u) + (2 * j + 1 < s.bin_hi ? (w >> 16) : 0u);
   }
+#endif
   return sum == s.c_hi;
 }
 
@@ -300,10 +320,28 @@ template <int MODE>
 __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3,
                                         uint32_t *pool, int lane) {
   if (MODE == MODE_HIST) {
+#ifndef LSK_GRID_NOSKIP
     const uint32_t um = min(min(u0, u1), min(u2, u3));
     if (!__ballot(um < s.hi_b)) return;
+#endif
     const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
     const uint32_t u[4] = {u0, u1, u2, u3};
+#if LSK_GRID_PAIRHIST
+    // every slot adds: in range to its bin, past the range (or past the 40 bins) to a bin
+    // at or above bin_hi / the trash row, which nothing reads. A 16-bit wrap (65536 adds to
+    // one bin in a pass) lands in a counter hist_consistent checks, or carries into the
+    // partner lane's same row: a checked counter of its, or one nothing reads.
+    const uint32_t hl = (uint32_t)lane & 31u, inc = 1u << (((uint32_t)lane & 32u) >> 1);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const uint32_t v = u[t];
+      const uint32_t b = min(__builtin_elementwise_sub_sat(v, lb) >> sh, (uint32_t)kBins);
+      atomicAdd(&pool[b * 32u + hl], inc);
+      s.c_hi += v < hb ? 1u : 0u;
+    }
+    (void)sh1;
+    return;
+#endif
 #ifdef LSK_GRID_BRANCHLESS
     // every slot adds (0 when out of range): no exec-mask round trip per candidate
 #pragma unroll
@@ -796,6 +834,7 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
       }
 #pragma unroll 4
       for (int j = 0; j < kPool / lsk::kWave; j++) pool[j * lsk::kWave + lane] = 0u;
+      if (kPool % lsk::kWave != 0 && lane < kPool % lsk::kWave) pool[kPool - kPool % lsk::kWave + lane] = 0u;
       if (!grid_pass<MODE_HIST>(s, G, ntree)) {
         gfail = true;
         break;
