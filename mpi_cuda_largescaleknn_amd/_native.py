@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 6  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 5  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -91,7 +91,7 @@ class KnnArgs(C.Structure):
 class GridView(C.Structure):
     _fields_ = [
         ("slots", vp),
-        ("pairs", vp),
+        ("pad_", vp),
         ("box", vp),
         ("inf4", vp),
         ("level", C.c_int32),
@@ -166,7 +166,6 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_knn_grid": ([C.POINTER(KnnArgs), C.POINTER(GridView), vp], i32),
         "lsk_hip_grid_build": ([vp, vp, i64, vp, i32, vp, vp], i32),
-        "lsk_hip_grid_pairs": ([vp, i64, vp, i64, vp], i32),
         "lsk_hip_key_levels": ([vp, i64, vp, vp], i32),
         "lsk_hip_grid_sq": ([vp, i64, vp, vp], i32),
         "lsk_hip_halo_mask": ([vp, i64, vp, vp, vp, i32, i32, vp, vp], i32),

@@ -252,7 +252,6 @@ __device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
 // Wave-uniform grid context.
 struct GridCtx {
   const float *pts;        // sorted points (packed float3, padded)
-  const float *pairs;      // the same points in pairs (x0 x1 y0 y1 z0 z1), padded
   const float *inf4;       // 4 x +inf (tail padding of a candidate batch)
   const uint4 *slots;      // [8^lc][64] grandchild runs (start, end, coords, -) in Hilbert order
   float ox, oy, oz;        // cube origin
@@ -446,118 +445,6 @@ __device__ __forceinline__ void eval4_tail(Lane &s, GridCtx &G, const Batch &b, 
   update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane);
 }
 
-// Pair-layout batches (LSK_GRID_PAIRS): the grid build keeps a second copy of the sorted
-// points with every two consecutive points interleaved per axis (x0 x1 y0 y1 z0 z1), so a
-// batch of 4 points starting at an EVEN index is 12 dwords at the same offset as in the
-// packed float3 array, and each axis of two candidates is one aligned SGPR pair. The
-// canonical d² of two candidates is then 6 packed-fp32 VALU ops (v_pk_add / v_pk_mul /
-// v_pk_fma, the query splatted through op_sel) instead of 12: per half the same IEEE
-// operations in the same order as lsk::dist2, hence the same bits.
-typedef float f2v __attribute__((ext_vector_type(2)));
-struct Batch2 {
-  f2v x01, y01, z01, x23, y23, z23;
-};
-__device__ __forceinline__ Batch2 load_batch2(lsk::cfloat_p P2, uint32_t b) {  // b even
-  const lsk::cfloat_p p = P2 + 3ull * (uint64_t)b;
-  return Batch2{f2v{p[0], p[1]}, f2v{p[2], p[3]}, f2v{p[4], p[5]},
-                f2v{p[6], p[7]}, f2v{p[8], p[9]}, f2v{p[10], p[11]}};
-}
-__device__ __forceinline__ f2v dist2v(f2v dx, f2v dy, f2v dz) {
-  return __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-}
-// m: wave-uniform mask of the batch's valid points (0xf: all; else a segment's odd head
-// or its tail): the others count nowhere.
-template <int MODE>
-__device__ __forceinline__ void eval4p(Lane &s, GridCtx &G, const Batch2 &b, uint32_t m) {
-  const f2v qx = f2v{s.qx, s.qx}, qy = f2v{s.qy, s.qy}, qz = f2v{s.qz, s.qz};
-  const f2v d01 = dist2v(qx - b.x01, qy - b.y01, qz - b.z01);
-  const f2v d23 = dist2v(qx - b.x23, qy - b.y23, qz - b.z23);
-  uint32_t u0 = fbits(d01.x), u1 = fbits(d01.y), u2 = fbits(d23.x), u3 = fbits(d23.y);
-  if (m != 0xfu) {
-    u0 = (m & 1u) ? u0 : ~0u;
-    u1 = (m & 2u) ? u1 : ~0u;
-    u2 = (m & 4u) ? u2 : ~0u;
-    u3 = (m & 8u) ? u3 : ~0u;
-  }
-  update4<MODE>(s, u0, u1, u2, u3, G.pool, G.lane);
-}
-
-#ifndef LSK_GRID_PAIRS
-#define LSK_GRID_PAIRS 1
-#endif
-
-#if LSK_GRID_PAIRS
-// process_cell_stream over the pair layout: batches start at even indices, so a segment
-// starting at an odd index masks its first slot (lo = the segment's first point).
-template <int MODE>
-__device__ __forceinline__ void process_cell_stream(Lane &s, GridCtx &G, const CellLoad &c, uint64_t need,
-                                                    uint64_t free) {
-  const lsk::cfloat_p P = lsk::as_const(G.pairs);
-  auto pop = [&](uint32_t &a, uint32_t &b) {
-    const uint32_t t0 = (uint32_t)__builtin_ctzll(need);
-    const uint64_t after = ~free >> t0;
-    const uint32_t len = after ? (uint32_t)__builtin_ctzll(after) : 64u - t0;
-    const uint64_t run = (len >= 64u ? ~0ull : ((1ull << len) - 1ull)) << t0;
-    const uint64_t in = need & run;
-    const uint32_t t1 = 63u - (uint32_t)__builtin_clzll(in);
-    need &= ~run;
-    a = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)c.a, (int)t0));
-    b = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)c.e, (int)t1));
-    G.segs++;
-  };
-  // mask of the batch at i (even) inside the segment [lo, e)
-  auto mask_of = [](uint32_t i, uint32_t lo, uint32_t e) -> uint32_t {
-    const uint32_t left = e - i;
-    return (0xfu << (lo - i)) & (left >= 4u ? 0xfu : ((1u << left) - 1u));
-  };
-  uint32_t lo, e;
-  pop(lo, e);
-  uint32_t i = lo & ~1u;
-  uint32_t chk = i + kSegCheck;
-  auto advance = [&](uint32_t &ni, uint32_t &nlo, uint32_t &ne) -> bool {
-    ni = i + 4u;
-    nlo = lo;
-    ne = e;
-    if (ni < e) return true;
-    if (!need) {
-      ni = i;  // (a dummy reload of the current batch: in flight, unused)
-      return false;
-    }
-    pop(nlo, ne);
-    ni = nlo & ~1u;
-    return true;
-  };
-  Batch2 A = load_batch2(P, i);
-  for (;;) {
-    uint32_t ni, nlo, ne;
-    bool more = advance(ni, nlo, ne);
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    Batch2 B = load_batch2(P, ni);
-    __builtin_amdgcn_sched_barrier(0);
-    eval4p<MODE>(s, G, A, mask_of(i, lo, e));
-    count_batch<MODE>(G);
-    if (!more) break;
-    i = ni;
-    lo = nlo;
-    e = ne;
-    more = advance(ni, nlo, ne);
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    A = load_batch2(P, ni);
-    __builtin_amdgcn_sched_barrier(0);
-    eval4p<MODE>(s, G, B, mask_of(i, lo, e));
-    count_batch<MODE>(G);
-    if (!more) break;
-    i = ni;
-    lo = nlo;
-    e = ne;
-    if (MODE == MODE_HIST && i >= chk) {
-      chk = i + kSegCheck;
-      shrink_all<MODE>(s, G);
-      if (!__ballot(s.state == ST_HIST && s.hi_b > 0u)) break;
-    }
-  }
-}
-#else
 // The candidates of one cell as ONE stream over its needed runs of grandchildren, 4 per
 // batch. Slots are in memory order, so a run of needed (or empty) slots is one
 // contiguous segment of the sorted array. The next batch's scalar loads — the next
@@ -629,8 +516,6 @@ __device__ __forceinline__ void process_cell_stream(Lane &s, GridCtx &G, const C
     }
   }
 }
-
-#endif  // LSK_GRID_PAIRS
 
 // Unrolled by two with separate A / B batch registers: a loop-carried copy of the batch
 // would make the compiler wait for the prefetch right after issuing it.
@@ -834,7 +719,6 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
 
   GridCtx G;
   G.pts = A.tree[0].pts;
-  G.pairs = V.pairs;
   G.inf4 = V.inf4;
   G.slots = (const uint4 *)V.slots;
   {
@@ -1133,30 +1017,6 @@ __global__ __launch_bounds__(256) void grid_build_kernel(const float *__restrict
   if (last) slot[1] = (uint32_t)(i + 1);
 }
 
-// Pair layout (see Batch2): thread j writes pair j = points 2j, 2j+1 (+inf past n).
-__global__ __launch_bounds__(256) void grid_pairs_kernel(const float *__restrict__ pts, int64_t n,
-                                                         int64_t npairs, float *__restrict__ pairs) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= npairs) return;
-  const float inf = __builtin_inff();
-  const int64_t i = 2 * j;
-  float a[3] = {inf, inf, inf}, b[3] = {inf, inf, inf};
-  if (i < n) {
-    a[0] = pts[3 * i];
-    a[1] = pts[3 * i + 1];
-    a[2] = pts[3 * i + 2];
-  }
-  if (i + 1 < n) {
-    b[0] = pts[3 * i + 3];
-    b[1] = pts[3 * i + 4];
-    b[2] = pts[3 * i + 5];
-  }
-  float2 *o = (float2 *)(pairs + 6 * j);
-  o[0] = make_float2(a[0], b[0]);
-  o[1] = make_float2(a[1], b[1]);
-  o[2] = make_float2(a[2], b[2]);
-}
-
 // counts[l] += number of i in [1, n) whose key prefix at level l (top 3l bits of the
 // 30-bit key) differs from key i-1's: distinct cells of level l = counts[l] + 1.
 // Grid-stride: per-thread counts in registers, wave sums, one atomic per level and block.
@@ -1232,18 +1092,6 @@ extern "C" int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorte
   return 0;
 }
 
-extern "C" int lsk_hip_grid_pairs(const float *sorted_pts, int64_t n, float *pairs, int64_t npairs,
-                                  void *stream) {
-  if (npairs < (n + 1) / 2) {
-    lsk::set_last_error("grid_pairs: npairs must be >= (n + 1) / 2");
-    return 1;
-  }
-  if (npairs <= 0) return 0;
-  grid_pairs_kernel<<<lsk_blocks(npairs, 256), 256, 0, (hipStream_t)stream>>>(sorted_pts, n, npairs, pairs);
-  LSK_CHECK_LAUNCH("grid_pairs");
-  return 0;
-}
-
 extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
@@ -1269,9 +1117,9 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
     return 1;
   }
   if (A.nq >= ((int64_t)1 << 32) || A.ntrees != 1 || A.groups || A.init_d2 ||
-      A.tree[0].n >= ((int64_t)1 << 32) || !grid || grid->level < 0 || grid->level > 8 || !grid->pairs) {
+      A.tree[0].n >= ((int64_t)1 << 32) || !grid || grid->level < 0 || grid->level > 8) {
     lsk::set_last_error("knn_grid: one tree (< 2^32 points, the queries' own), no groups / init_d2, "
-                        "grid level in [0, 8], pair layout");
+                        "grid level in [0, 8]");
     return 1;
   }
   const int64_t ngroups = (A.nq + 63) / 64;

@@ -146,8 +146,7 @@ int lsk_hip_knn_exact(const lsk_knn_args *args, const uint32_t *list, const uint
 // indexed by the Morton code of their coordinates.
 typedef struct lsk_grid_view {
   const uint32_t *slots;  // [8^level * 64][4]
-  const float *pairs;     // [(n + 1) / 2 + 32][6] the sorted points, two at a time per axis
-                          // (x0 x1 y0 y1 z0 z1; lsk_hip_grid_pairs), +inf padded
+  const uint32_t *pad_;   // (unused)
   const float *box;       // [8] device: the box of the sort keys (lo.xyz, hi.xyz, scale, extent)
   const float *inf4;      // [4] device: +inf (unused padding source)
   int32_t level;
@@ -155,10 +154,6 @@ typedef struct lsk_grid_view {
 } lsk_grid_view;
 int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorted_keys, int64_t n, const float *box,
                        int32_t level, uint32_t *slots, void *stream);
-// Pair layout of the sorted points for the grid kernel's packed-fp32 candidate math:
-// pairs[6j .. 6j+5] = (x_2j, x_2j+1, y_2j, y_2j+1, z_2j, z_2j+1); npairs >= (n + 1) / 2,
-// points past n (pad) are +inf.
-int lsk_hip_grid_pairs(const float *sorted_pts, int64_t n, float *pairs, int64_t npairs, void *stream);
 // counts[l] (l = 1..10, 11 slots, zeroed here) = number of adjacent sorted keys whose level-l
 // prefixes differ (distinct level-l cells = counts[l] + 1).
 int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream);

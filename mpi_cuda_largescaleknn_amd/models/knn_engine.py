@@ -75,13 +75,12 @@ class GridIndex:
                              # grandchildren's runs of the sorted array in curve order
     level: int               # cell level (grandchildren at level + 2)
     box: torch.Tensor        # the cube of the sort keys (device)
-    pairs: torch.Tensor      # the sorted points two at a time per axis (K.grid_pairs)
     inf4: torch.Tensor | None = None  # 4 x +inf on the device (candidate padding)
 
     def view(self) -> tuple:
         if self.inf4 is None:
             self.inf4 = torch.full((4,), math.inf, dtype=torch.float32, device=self.slots.device)
-        return (self.slots, self.level, self.box, self.inf4, self.pairs)
+        return (self.slots, self.level, self.box, self.inf4)
 
 
 @dataclass
@@ -188,7 +187,7 @@ def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
         mean = n / max(1, distinct[g])
         if seen > GRID_CROWD * (mean + 1.0):
             return None
-    return GridIndex(slots, g - 2, index.box, K.grid_pairs(index.pts, n))
+    return GridIndex(slots, g - 2, index.box)
 
 
 HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key

@@ -353,8 +353,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_count = _ptr(count)
     a.fail_cap = cap
     if impl == "grid":
-        slots, level, gbox, inf4, pairs = grid
-        gv = GridView(_ptr(slots), _ptr(pairs), _ptr(gbox), _ptr(inf4), int(level), 0)
+        slots, level, gbox, inf4 = grid
+        gv = GridView(_ptr(slots), None, _ptr(gbox), _ptr(inf4), int(level), 0)
         check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
     else:
         check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
@@ -385,16 +385,6 @@ def grid_build(sorted_pts: torch.Tensor, sorted_keys: torch.Tensor, n: int, box:
     check(_native.hip().lsk_hip_grid_build(_ptr(sorted_pts), _ptr(sorted_keys), n, _ptr(box), level, _ptr(slots),
                                            _stream(sorted_pts)), "grid_build")
     return slots
-
-
-def grid_pairs(sorted_pts: torch.Tensor, n: int) -> torch.Tensor:
-    """The sorted points two at a time per axis (x0 x1 y0 y1 z0 z1) for the grid kernel's
-    packed-fp32 candidate math: float32 [(n + 1) // 2 + 32, 6], +inf past n."""
-    npairs = (n + 1) // 2 + 32
-    pairs = torch.empty((npairs, 6), dtype=torch.float32, device=sorted_pts.device)
-    check(_native.hip().lsk_hip_grid_pairs(_ptr(sorted_pts), n, _ptr(pairs), npairs, _stream(sorted_pts)),
-          "grid_pairs")
-    return pairs
 
 
 def grid_sq(slots: torch.Tensor) -> int:

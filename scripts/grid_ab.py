@@ -36,8 +36,7 @@ if a.levels:
     from mpi_cuda_largescaleknn_amd.ops import kernels as K  # noqa: E402
     skeys, _ = K.morton(idx.pts[:n], idx.box, with_iota=False)  # keys of the sorted points
     for g in [int(x) for x in a.levels.split(",")]:  # finest level (cells at g - 2)
-        grids[f"grid-L{g}"] = E.GridIndex(K.grid_build(idx.pts, skeys, n, idx.box, g - 2), g - 2, idx.box,
-                                          idx.grid.pairs)
+        grids[f"grid-L{g}"] = E.GridIndex(K.grid_build(idx.pts, skeys, n, idx.box, g - 2), g - 2, idx.box)
 res = {}
 for impl in list(grids) + ["rows"]:
     idx.grid = grids.get(impl)

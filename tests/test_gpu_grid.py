@@ -114,17 +114,3 @@ def test_grid_auto_skips_crowded_data():
         assert idx.grid is not None
     finally:
         E.GRID = old
-
-
-@pytest.mark.parametrize("n", [1, 2, 7, 1000])
-def test_grid_pairs_layout(n):
-    """Pair layout of the sorted points (packed-fp32 candidates of knn_grid): row j holds
-    points 2j and 2j+1 per axis (x0 x1 y0 y1 z0 z1), +inf past n."""
-    p = uniform(n, seed=n).to(DEV)
-    pairs = K.grid_pairs(p, n).cpu()
-    npairs = (n + 1) // 2 + 32
-    assert pairs.shape == (npairs, 6)
-    ref = torch.full((2 * npairs, 3), math.inf)
-    ref[:n] = p.cpu()
-    ref = ref.view(npairs, 2, 3).transpose(1, 2).reshape(npairs, 6)
-    assert torch.equal(pairs, ref)
