@@ -54,7 +54,7 @@ constexpr int kBins = 40;                 // 16-bit bins, two per LDS dword (as 
 // (values past the range go to a trash row, kBins); else (as knn_rows) bins 2j and 2j+1
 // of one lane share a dword.
 #ifndef LSK_GRID_PAIRHIST
-#define LSK_GRID_PAIRHIST 0
+#define LSK_GRID_PAIRHIST 1
 #endif
 #if LSK_GRID_PAIRHIST
 constexpr int kPool = (kBins + 1) * 32;   // dwords per wave: histogram + trash row, or collect pool
@@ -117,6 +117,12 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
   s.hi_b = (uint32_t)hi;
   s.bin_hi = hi > lo_b ? (int32_t)((hi - lo_b + ((1ull << shift) - 1)) >> shift) : 0;
   s.c_hi = 0;
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(uint32_t *p) { return (uint32_t)(uintptr_t)(lds_u32 *)p; }
+__device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
+  __atomic_fetch_add((lds_u32 *)(uintptr_t)addr, v, __ATOMIC_RELAXED);
 }
 
 __device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
@@ -261,6 +267,7 @@ struct GridCtx {
   uint32_t lc;             // cell level
   float wlx, wly, wlz, whx, why, whz;  // box of the wave's queries
   uint32_t *pool;
+  uint32_t trash;          // LDS byte address of this lane's trash-row counter (opaque)
   int lane;
   uint32_t k;
   uint32_t evals, cells_n, segs;
@@ -318,7 +325,7 @@ __device__ __forceinline__ float cull_r2(const Lane &s, const GridCtx &G) {
 
 template <int MODE>
 __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3,
-                                        uint32_t *pool, int lane) {
+                                        uint32_t *pool, int lane, uint32_t hist_trash) {
   if (MODE == MODE_HIST) {
 #ifndef LSK_GRID_NOSKIP
     const uint32_t um = min(min(u0, u1), min(u2, u3));
@@ -327,17 +334,24 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
     const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
     const uint32_t u[4] = {u0, u1, u2, u3};
 #if LSK_GRID_PAIRHIST
-    // every slot adds: in range to its bin, past the range (or past the 40 bins) to a bin
-    // at or above bin_hi / the trash row, which nothing reads. A 16-bit wrap (65536 adds to
-    // one bin in a pass) lands in a counter hist_consistent checks, or carries into the
+    // every slot adds, without a branch: a value below hi_b to its bin (< bin_hi), any
+    // other (past the range, or a lane not histogramming: hi_b = 0) to the trash row kBins,
+    // which nothing reads; the compare also counts c_hi. A 16-bit wrap (65536 adds to one
+    // bin in a pass) lands in a counter hist_consistent checks, or carries into the
     // partner lane's same row: a checked counter of its, or one nothing reads.
-    const uint32_t hl = (uint32_t)lane & 31u, inc = 1u << (((uint32_t)lane & 32u) >> 1);
+    // 6 VALU per candidate (sub_sat, shift, compare, select, address, carry-add) and no
+    // exec-mask round trip: 0.0885 vs 0.0955 s on 1e8 uniform points, k = 100.
+    // (byte addresses: the row address is one shift-add, the trash address an opaque
+    // per-lane value, so the select picks between addresses, not bin indices)
+    const uint32_t inc = 1u << (((uint32_t)lane & 32u) >> 1);
+    const uint32_t row0 = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u, trash = hist_trash;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const uint32_t v = u[t];
-      const uint32_t b = min(__builtin_elementwise_sub_sat(v, lb) >> sh, (uint32_t)kBins);
-      atomicAdd(&pool[b * 32u + hl], inc);
-      s.c_hi += v < hb ? 1u : 0u;
+      const bool in = v < hb;
+      const uint32_t a = in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash;
+      lds_add(a, inc);
+      s.c_hi += in ? 1u : 0u;
     }
     (void)sh1;
     return;
@@ -412,7 +426,7 @@ __device__ __forceinline__ void eval4(Lane &s, GridCtx &G, const Batch &b) {
   const uint32_t u1 = fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1));
   const uint32_t u2 = fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2));
   const uint32_t u3 = fbits(lsk::dist2(s.qx - b.x3, s.qy - b.y3, s.qz - b.z3));
-  update4<MODE>(s, u0, u1, u2, u3, G.pool, G.lane);
+  update4<MODE>(s, u0, u1, u2, u3, G.pool, G.lane, G.trash);
 }
 
 // The 64 grandchild slots of one level-lc cell, fetched ahead of use (one 16-byte vector
@@ -442,7 +456,7 @@ __device__ __forceinline__ void eval4_tail(Lane &s, GridCtx &G, const Batch &b, 
   const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
   const uint32_t u1 = left > 1u ? fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1)) : ~0u;
   const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
-  update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane);
+  update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane, G.trash);
 }
 
 // The candidates of one cell as ONE stream over its needed runs of grandchildren, 4 per
@@ -558,7 +572,7 @@ __device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0
     const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
     const uint32_t u1 = left > 1u ? fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1)) : ~0u;
     const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
-    update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane);
+    update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane, G.trash);
   }
   G.evals += (i1 - i0 + 3u) & ~3u;  // (an early stop counts the whole segment)
   G.segs++;
@@ -735,6 +749,8 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   G.lc = (uint32_t)V.level;
   G.pool = pool;
   G.lane = lane;
+  G.trash = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u + (uint32_t)kBins * 128u;
+  asm volatile("" : "+v"(G.trash));
   G.k = k;
   G.evals = G.cells_n = G.segs = 0;
 #ifdef LSK_GRID_PROFILE

@@ -573,8 +573,9 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
 # --------------------------------------------------------------------------- entrypoints
 # Single-rank runs can let the k-NN kernel write the distances straight into pinned host
 # memory (random 4-byte PCIe writes at perm[q], hidden under the kernel) instead of a
-# device buffer + copy. The writes sustain ~0.9-1e9 points/s: they hide under the kernel
-# only when it is slow enough per point, i.e. from k ~ 48 (1e8 uniform points on one
+# device buffer + copy. The writes sustain ~0.9-1e9 points/s: they hide under the bucket-
+# tree kernel only when it is slow enough per point, i.e. from k ~ 48 (the cell-grid
+# kernel is faster than the writes at k = 100: local_query keeps its output on the device) (1e8 uniform points on one
 # MI355X, step ms copy/direct: k=16 118/172, k=48 141/135, k=64 151/145, k=100
 # 176/170; 1e7 k=16 12.5/17.9; profiles/r1_v20/direct_out_ab.txt).
 DIRECT_OUT_MIN_K = 48
@@ -697,8 +698,17 @@ def local_query(index: E.LocalIndex, hint2, cfg: E.KnnConfig, info: RunInfo | No
     (fused scatter) into `out` (see unordered_knn). `deferred`: as in knn_engine.query."""
     info = info or RunInfo(PhaseTimer(False, index.device))
     out = _check_out(out, index.n, index.pts)
-    E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out,
-            deferred=deferred)
+    host = out.device.type == "cpu" and index.pts.device.type == "cuda"
+    if host and index.grid is not None and deferred is None:
+        # the cell-grid kernel outruns the random 4-byte PCIe writes of a direct output
+        # (1B uniform, k=100: 1321 ms direct vs ~950 ms for the kernel alone): write the
+        # device and copy the 4 B/point back in one transfer
+        dev_out = torch.empty(index.n, dtype=torch.float32, device=index.device)
+        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=dev_out)
+        out.copy_(dev_out, non_blocking=True)
+    else:
+        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out,
+                deferred=deferred)
     info.timer.mark("knn_local")
     return out
 
