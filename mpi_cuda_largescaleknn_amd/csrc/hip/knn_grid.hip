@@ -73,7 +73,10 @@ constexpr uint32_t kShift0 = 20;          // 1/8 octave of d² per bin
 constexpr uint32_t kMaxPasses = 24;
 constexpr uint32_t kUnknown = 0xffffffffu;
 constexpr uint32_t kNaNBits = 0x7fc00000u;
-constexpr float kEstCalib = 0.8f;
+#ifndef LSK_GRID_EST_CALIB
+#define LSK_GRID_EST_CALIB 0.8f
+#endif
+constexpr float kEstCalib = LSK_GRID_EST_CALIB;  // first-range estimate scale (d²)
 
 // LSK_GRID_PROFILE builds (tuning only): shader-clock cycles per wave in candidate
 // processing / cell enumeration of each pass kind, and the whole wave, into

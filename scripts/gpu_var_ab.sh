@@ -1,11 +1,13 @@
-# A/B of kernel library variants (scripts/build_variant.py): grid tests on each, then the
-# 1e8 k-NN pass (knn_only, 3 reps) base vs variants. VARIANTS="a b ..."
+# k-NN pass of library variants ($VARIANTS, scripts/build_variant.py) at 1e8 against the
+# default, after the grid tests on each variant
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+source scripts/gpu_check.sh
 X=$PWD/mpi_cuda_largescaleknn_amd/lib/exp
-for v in $VARIANTS; do
-  LSKNN_HIP_LIB=$X/liblsknn_hip_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_grid.py > gpurun_out/vt_$v.log 2>&1 || { echo "$v tests failed"; tail -20 gpurun_out/vt_$v.log; exit 1; }
-  echo "== $v tests: $(tail -1 gpurun_out/vt_$v.log)"
+for v in base $VARIANTS; do
+  if [ $v = base ]; then L=""; else L=$X/liblsknn_hip_$v.so; fi
+  LSKNN_HIP_LIB=$L run 200 var_tests_$v.log python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_gpu_grid.py
+  grep -q " passed" gpurun_out/var_tests_$v.log && ! grep -q "failed" gpurun_out/var_tests_$v.log || exit 1
+  LSKNN_HIP_LIB=$L run 300 var_knn_$v.log python -u scripts/knn_only.py --points ${N:-1e8} --reps 3 --grid 1
 done
-N=${N:-1e8} VARIANTS="$VARIANTS" bash scripts/gpu_grid_variants.sh
