@@ -23,16 +23,22 @@
 //    addresses through the constant address space): the candidates arrive in SGPRs and
 //    every VALU op of the canonical d² takes them as an operand — 6 VALU per candidate and
 //    lane, no broadcast, no per-row queues or logs; the next batch's loads (across segment
-//    boundaries) are issued before the current batch is computed.
+//    boundaries) are issued before the current batch is computed;
+//  * the histogram update is branch-free (LSK_GRID_PAIRHIST): lanes l and l+32 share one
+//    dword per bin row, every candidate adds to its bin or to a per-lane trash row through
+//    a select between two LDS addresses, and the select's compare also counts c_hi —
+//    6 VALU per candidate, no exec-mask round trip. The kernel is VALU-cycle bound: a
+//    wave64 op takes 2 cycles on the 32-lane SIMD, packed f32 ops take 4 (no gain), and an
+//    exec-masked half wave costs a full op (profiles/r3_pairs, profiles/r3_hist).
 //
 // Every cull is conservative: cell boxes are the quantisation intervals widened by a
 // few ulps of the cube, the radius is inflated by 2^-16 (relative) over the largest lane
 // bound, so a skipped point always has canonical d² >= every lane's bound.
 //
 // Measured on one MI355X, uniform points, k = 100, this pass vs the bucket-tree kernel on
-// the same index (scripts/grid_ab.py, bit-identical outputs): 1e8 0.108 vs 0.124 s (with
-// sub-cells, before the 64-slot cells), 1B 1.20 vs 1.29 s; GRID=auto keeps clustered,
-// planar, duplicate and mixed-scale data on knn_rows (knn_engine.grid_applies).
+// the same index (bit-identical outputs): 1e8 0.088 vs 0.125 s, 1B 0.932 vs 1.29 s
+// (profiles/r3_hist, profiles/r3_s2); GRID=auto keeps clustered, planar, duplicate and
+// mixed-scale data on knn_rows (knn_engine.grid_applies).
 #include "dev.h"
 
 namespace {
