@@ -114,3 +114,13 @@ def test_grid_auto_skips_crowded_data():
         assert idx.grid is not None
     finally:
         E.GRID = old
+
+
+def test_grid_knn_large_k_counter_wraps():
+    """k in the thousands: a histogram pass makes tens of thousands of adds per lane, so
+    16-bit bin counters (two lanes per dword in the paired-lane layout) can wrap; every
+    wrap must be caught (checksum -> exact backstop) and the output stay exact."""
+    p = uniform(120_000, seed=5)
+    for k in (2000, 6000):
+        got, _, st = grid_knn(p, k)
+        assert torch.equal(got, oracle(p, k)), (k, st.counters)
