@@ -75,7 +75,18 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 // Measured on 1e8 uniform points, k=100.
 constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
 static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
+// LSK_ROWS_PAIRHIST (default, as knn_grid.hip): lanes l and l+32 share a dword (low /
+// high half) of each bin row, so a lane's increment is a per-lane constant and every
+// candidate adds without a branch — in range to its bin, otherwise to a trash row (kBins)
+// that nothing reads; else bins 2j and 2j+1 of one lane share a dword (exec-masked adds).
+#ifndef LSK_ROWS_PAIRHIST
+#define LSK_ROWS_PAIRHIST 1
+#endif
+#if LSK_ROWS_PAIRHIST
+constexpr int kPool = (kBins + 1) * 32;  // dwords per wave: histogram + trash row, or collect pool
+#else
 constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
+#endif
 // 16 bins (2 octaves of d²) above the estimate: with Hilbert-sorted groups fewer
 // overflow retries than 12 (1e8 uniform, k=100: 0.155 vs 0.159 s; 8: 0.179 s)
 // (with the blended estimate below: 12 bins = 1.5 octaves; 1e8 uniform, k=100: 8 bins
@@ -181,7 +192,17 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
 }
 
 __device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
+#if LSK_ROWS_PAIRHIST
+  return (pool[b * 32u + ((uint32_t)lane & 31u)] >> (((uint32_t)lane & 32u) >> 1)) & 0xffffu;
+#else
   return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
+#endif
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(uint32_t *p) { return (uint32_t)(uintptr_t)(lds_u32 *)p; }
+__device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
+  __atomic_fetch_add((lds_u32 *)(uintptr_t)addr, v, __ATOMIC_RELAXED);
 }
 
 __device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *pool, int lane) {
@@ -286,7 +307,8 @@ __device__ __forceinline__ uint32_t cand(const Lane &s, float px, float py, floa
 }
 
 template <int MODE, int G>
-__device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_t *pool, int lane) {
+__device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_t *pool, int lane,
+                                        uint32_t trash) {
   uint32_t umin = u[0];
 #pragma unroll
   for (int t = 1; t < G; t++) umin = min(umin, u[t]);
@@ -306,6 +328,22 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
     // bin = sat(v - lo_b) >> shift (< 64 for every v < hi_b); bins 2j, 2j+1 share the
     // lane's dword j as two 16-bit counters
     const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
+#if LSK_ROWS_PAIRHIST
+    // branch-free: a value below hi_b to its bin, any other to the lane's trash row
+    // (`trash`, an opaque per-lane LDS address, so the select is between addresses); the
+    // compare also counts c_hi. 6 VALU per candidate, no exec-mask round trip.
+    const uint32_t inc = 1u << (((uint32_t)lane & 32u) >> 1);
+    const uint32_t row0 = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u;
+    (void)sh1;
+#pragma unroll
+    for (int t = 0; t < G; t++) {
+      const uint32_t v = u[t];
+      const bool in = v < hb;
+      lds_add(in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash, inc);
+      s.c_hi += in ? 1u : 0u;
+    }
+    if (true) return lane_in;
+#endif
 #pragma unroll
     for (int t = 0; t < G; t++) {
       const uint32_t v = u[t];
@@ -340,29 +378,29 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
 // The 16 candidates of this lane's row quarter (lane i of the row holds candidate i).
 template <int MODE>
 __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz, uint32_t cnt,
-                                          uint32_t *pool, int lane, uint32_t k, bool &crowd) {
+                                          uint32_t *pool, int lane, uint32_t trash, uint32_t k, bool &crowd) {
   bool lane_in;
   // groups of 4 candidates: 4 fewer live VGPRs in the hot loop than groups of 8
   {
     uint32_t u[4] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
                      cand<3>(s, px, py, pz)};
-    lane_in = update8<MODE, 4>(s, u, pool, lane);
+    lane_in = update8<MODE, 4>(s, u, pool, lane, trash);
   }
   {
     uint32_t u[4] = {cand<4>(s, px, py, pz), cand<5>(s, px, py, pz), cand<6>(s, px, py, pz),
                      cand<7>(s, px, py, pz)};
-    lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
+    lane_in = update8<MODE, 4>(s, u, pool, lane, trash) || lane_in;
   }
   if (__ballot(cnt > 8u)) {
     {
       uint32_t u[4] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
                        cand<11>(s, px, py, pz)};
-      lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
+      lane_in = update8<MODE, 4>(s, u, pool, lane, trash) || lane_in;
     }
     {
       uint32_t u[4] = {cand<12>(s, px, py, pz), cand<13>(s, px, py, pz), cand<14>(s, px, py, pz),
                        cand<15>(s, px, py, pz)};
-      lane_in = update8<MODE, 4>(s, u, pool, lane) || lane_in;
+      lane_in = update8<MODE, 4>(s, u, pool, lane, trash) || lane_in;
     }
   }
   if (MODE == MODE_HIST && __ballot(s.c_hi >= k)) crowd = __ballot(hist_shrink(s, pool, lane, k)) != 0 || crowd;
@@ -373,6 +411,7 @@ struct WaveCtx {
   WaveLds *L;
   uint32_t *rl;
   uint32_t rcap;
+  uint32_t trash;  // LDS byte address of this lane's trash-row counter (opaque; PAIRHIST)
   int lane, row;
   uint32_t k;
   uint32_t g;
@@ -481,7 +520,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
 #ifdef LSK_PROFILE
     s.pband = false;
 #endif
-    const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.k, W.crowd);
+    const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.trash, W.k, W.crowd);
 #ifdef LSK_PROFILE
     if (MODE == MODE_HIST) {
       const uint32_t re = row_bits(__ballot(ccnt > 0u)), ri = row_bits(__ballot(lin));
@@ -1019,10 +1058,14 @@ constexpr uint32_t kNaNBits = 0x7fc00000u;
 __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *pool, int lane) {
   uint32_t sum = 0;
 #pragma unroll
+#if LSK_ROWS_PAIRHIST
+  for (int b = 0; b < kBins; b++) sum += b < s.bin_hi ? hist_read(pool, (uint32_t)b, lane) : 0u;
+#else
   for (int j = 0; j < kBins / 2; j++) {
     const uint32_t w = pool[j * lsk::kWave + lane];
     sum += (2 * j < s.bin_hi ? (w & 0xffffu) : 0u) + (2 * j + 1 < s.bin_hi ? (w >> 16) : 0u);
   }
+#endif
   return sum == s.c_hi;
 }
 
@@ -1049,6 +1092,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   W.rcap = RCAP;
   W.lane = lane;
   W.row = lane >> 4;
+  W.trash = lds_addr(W.L->pool) + ((uint32_t)lane & 31u) * 4u + (uint32_t)kBins * 128u;
+  asm volatile("" : "+v"(W.trash));
   W.k = k;
   W.g = g;
   W.seed = A.seed;
@@ -1202,6 +1247,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
       }
 #pragma unroll 8
       for (int j = 0; j < kPool / lsk::kWave; j++) W.L->pool[j * lsk::kWave + lane] = 0u;
+      if (kPool % lsk::kWave != 0 && lane < kPool % lsk::kWave)
+        W.L->pool[kPool - kPool % lsk::kWave + lane] = 0u;
       // pass 1 walks and logs; later passes replay the log when it is complete
       W.logging = first;
       if (first) W.log_ok = true;
