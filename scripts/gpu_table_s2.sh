@@ -10,6 +10,5 @@ run 300 t2_100m_pre.log python -u bench.py --points 1e8 --steps 10 --warmup 3 --
 LSKNN_GRID=auto run 400 t2_robust_auto.log python -u scripts/dist_robustness.py 20000000 100 16
 HIP_HOST_COHERENT=0 run 400 t2_noncoh_1b.log python -u bench.py --steps 8 --warmup 2 --verify 64
 source scripts/gpu_check.sh
-for c in 600 300 0; do
-  LSKNN_OUT_PACE_MS=$c run 400 pace_$c.log python -u bench.py --steps 8 --warmup 2 --verify 64
-done
+# (the result-copy pacing runs of this script used LSKNN_OUT_PACE_MS, removed after they
+#  measured slower: profiles/r3_s2/README.txt)
