@@ -373,6 +373,7 @@ def main():
                 "hip_graph": graph is not None,
                 "pipelined": pipelined,
                 "heavy_cells_unrefined": heavy_unrefined,
+                "knn_kernels": sorted(E.KERNELS_USED),
                 "all_finite": finite,
                 "sampled_exact": (f"{check['exact']}/{check['samples']}" if check else None),
             },

@@ -362,6 +362,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
         if groups is None:
             out.copy_(K.kth_cpu(pts, index.pts[:n], cfg.k, cfg.cut2))
             rows = None
+            KERNELS_USED.add("cpu")
         else:
             g = groups[:ngroups].to(torch.int64)
             rows = (g[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
@@ -380,6 +381,8 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     impl = KNN_IMPL
     use_grid = (impl == "rows" and index.grid is not None and len(trees) == 1 and groups is None
                 and init_d2 is None and cfg.k <= K.ROWS_MAX_K)
+    if groups is None:  # (a whole-set pass, not a halo re-query)
+        KERNELS_USED.add("grid" if use_grid else impl)
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
                    grid=index.grid.view() if use_grid else None, **kw)
@@ -412,6 +415,11 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     else:
         check()
     return out if want_d2 else final_out
+
+
+# k-NN kernels the whole-set passes of this process used ("grid", "rows", "exact"): the
+# bench reports them next to its number
+KERNELS_USED: set = set()
 
 
 def settle(deferred: list) -> bool:
