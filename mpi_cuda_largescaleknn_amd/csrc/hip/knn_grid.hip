@@ -68,11 +68,13 @@ constexpr int kPool = (kBins + 1) * 32;   // dwords per wave: histogram + trash 
 constexpr int kPool = kBins / 2 * 64;     // dwords per wave: histogram, or collect pool
 #endif
 // LSK_GRID_ROWCULL: a grandchild is needed when it lies within the cull radius of one of
-// the wave's four 16-query ROWS (each with its own box and radius) instead of the whole
-// wave's box and largest radius: the union of the rows' regions is smaller (1e7 uniform,
-// k = 100: 0.915x the candidates, scripts/sim_row_culling.py); 4 gap tests per grandchild.
+// the wave's four 16-query ROWS (each with its own box and radius, kept in LDS) instead of
+// the whole wave's box and largest radius: the union of the rows' regions is smaller
+// (0.918x the evaluations at 1e8 uniform, k = 100; 4 gap tests per grandchild): 0.088 ->
+// 0.085 s, 1B stream 1005 Mpts/s (profiles/r3_rowcull). With the row boxes in SGPRs the
+// extra pressure put spill reloads into the candidate loop and it was slower (0.091 s).
 #ifndef LSK_GRID_ROWCULL
-#define LSK_GRID_ROWCULL 0
+#define LSK_GRID_ROWCULL 1
 #endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
@@ -283,8 +285,9 @@ struct GridCtx {
   uint32_t lc;             // cell level
   float wlx, wly, wlz, whx, why, whz;  // box of the wave's queries
 #if LSK_GRID_ROWCULL
-  float rb[4][6];          // boxes of the wave's 4 rows of 16 queries (lo xyz, hi xyz)
-  float r2r[4];            // their squared cull radii (cull_r2)
+  float *rbox;             // LDS, per row r: [8r..8r+5] box of its 16 queries (lo xyz, hi
+                           // xyz), [8r+6] its squared cull radius (cull_r2); read per cell
+                           // (in SGPRs they pushed spill reloads into the candidate loop)
 #endif
   uint32_t *pool;
   uint32_t trash;          // LDS byte address of this lane's trash-row counter (opaque)
@@ -350,14 +353,13 @@ __device__ __forceinline__ float cull_r2(const Lane &s, GridCtx &G) {
   v = fmaxf(v, dpp_f<0x4E>(v));
   v = fmaxf(v, dpp_f<0x124>(v));
   v = fmaxf(v, dpp_f<0x128>(v));
-  float m = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16 * r));
-    G.r2r[r] = inflate_r2(b, G.eps);
-    m = fmaxf(m, G.r2r[r]);
-  }
-  return m;
+  const float r2 = inflate_r2(v, G.eps);  // this lane's row's radius
+  if ((G.lane & 15) == 0) G.rbox[(G.lane >> 4) * 8 + 6] = r2;
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 0);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 32);
+  const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 48);
+  return __uint_as_float(max(max(a, b), max(c, d)));
 #else
   return inflate_r2(wave_max_nonneg(lane_bound<MODE>(s)), G.eps);
 #endif
@@ -639,9 +641,9 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
   bool in_any = false;
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    const float g2 = lsk::dist2(gap1(lx, hx, G.rb[r][0], G.rb[r][3]), gap1(ly, hy, G.rb[r][1], G.rb[r][4]),
-                                gap1(lz, hz, G.rb[r][2], G.rb[r][5]));
-    in_any = in_any || g2 <= G.r2r[r];
+    const float *b = G.rbox + 8 * r;
+    const float g2 = lsk::dist2(gap1(lx, hx, b[0], b[3]), gap1(ly, hy, b[1], b[4]), gap1(lz, hz, b[2], b[5]));
+    in_any = in_any || g2 <= b[6];
   }
   const uint64_t need = __ballot(ne && in_any);
 #else
@@ -774,7 +776,11 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
 }
 
 __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
+#if LSK_GRID_ROWCULL
+  __shared__ uint32_t lds[kWPB][kPool + 32];
+#else
   __shared__ uint32_t lds[kWPB][kPool];
+#endif
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
   const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
@@ -806,6 +812,9 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   G.lc = (uint32_t)V.level;
   G.pool = pool;
   G.lane = lane;
+#if LSK_GRID_ROWCULL
+  G.rbox = (float *)(pool + kPool);
+#endif
   G.trash = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u + (uint32_t)kBins * 128u;
   asm volatile("" : "+v"(G.trash));
   G.k = k;
@@ -843,11 +852,8 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
       hi = fmaxf(hi, dpp_f<0x4E>(hi));
       hi = fmaxf(hi, dpp_f<0x124>(hi));
       hi = fmaxf(hi, dpp_f<0x128>(hi));
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        G.rb[r][a] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lo), 16 * r));
-        G.rb[r][3 + a] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi), 16 * r));
-      }
+      if ((lane & 15) == a) G.rbox[(lane >> 4) * 8 + a] = lo;
+      if ((lane & 15) == 3 + a) G.rbox[(lane >> 4) * 8 + 3 + a] = hi;
     }
   }
 #endif
