@@ -76,6 +76,24 @@ constexpr int kPool = kBins / 2 * 64;     // dwords per wave: histogram, or coll
 #ifndef LSK_GRID_ROWCULL
 #define LSK_GRID_ROWCULL 1
 #endif
+// (LSK_GRID_ROWCULL=2: eight groups of 8 queries instead of four rows of 16)
+constexpr int kCullGroups = LSK_GRID_ROWCULL == 2 ? 8 : 4;
+constexpr int kCullLanes = 64 / kCullGroups;
+
+// max / min inside each cull group (DPP: quads, then the half-row or the row); every lane
+// of a group ends with the group's value
+__device__ __forceinline__ float group_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false)));
+  if (kCullGroups == 8) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false)));
+  } else {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)));
+  }
+  return v;
+}
+__device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -348,13 +366,10 @@ template <int MODE>
 __device__ __forceinline__ float cull_r2(const Lane &s, GridCtx &G) {
 #if LSK_GRID_ROWCULL
   // row maxima (DPP inside the 16-lane rows), each row's radius, the wave's = the largest
-  float v = lane_bound<MODE>(s);
-  v = fmaxf(v, dpp_f<0xB1>(v));
-  v = fmaxf(v, dpp_f<0x4E>(v));
-  v = fmaxf(v, dpp_f<0x124>(v));
-  v = fmaxf(v, dpp_f<0x128>(v));
-  const float r2 = inflate_r2(v, G.eps);  // this lane's row's radius
-  if ((G.lane & 15) == 0) G.rbox[(G.lane >> 4) * 8 + 6] = r2;
+  float v = group_max(lane_bound<MODE>(s));
+  float r2 = inflate_r2(v, G.eps);  // this lane's group's radius
+  if ((G.lane & (kCullLanes - 1)) == 0) G.rbox[(G.lane / kCullLanes) * 8 + 6] = r2;
+  if (kCullGroups == 8) r2 = fmaxf(r2, dpp_f<0x128>(r2));  // pairs of groups -> rows
   const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 0);
   const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 16);
   const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 32);
@@ -640,7 +655,7 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
   cell_span(G, G.oz, c.xyz >> 20, sh, last, lz, hz);
   bool in_any = false;
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
+  for (int r = 0; r < kCullGroups; r++) {
     const float *b = G.rbox + 8 * r;
     const float g2 = lsk::dist2(gap1(lx, hx, b[0], b[3]), gap1(ly, hy, b[1], b[4]), gap1(lz, hz, b[2], b[5]));
     in_any = in_any || g2 <= b[6];
@@ -777,7 +792,7 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
 
 __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
 #if LSK_GRID_ROWCULL
-  __shared__ uint32_t lds[kWPB][kPool + 32];
+  __shared__ uint32_t lds[kWPB][kPool + 8 * kCullGroups];
 #else
   __shared__ uint32_t lds[kWPB][kPool];
 #endif
@@ -843,17 +858,9 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
     const float q3[3] = {s.qx, s.qy, s.qz};
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-      float lo = valid ? q3[a] : inf, hi = valid ? q3[a] : -inf;
-      lo = fminf(lo, dpp_f<0xB1>(lo));
-      lo = fminf(lo, dpp_f<0x4E>(lo));
-      lo = fminf(lo, dpp_f<0x124>(lo));
-      lo = fminf(lo, dpp_f<0x128>(lo));
-      hi = fmaxf(hi, dpp_f<0xB1>(hi));
-      hi = fmaxf(hi, dpp_f<0x4E>(hi));
-      hi = fmaxf(hi, dpp_f<0x124>(hi));
-      hi = fmaxf(hi, dpp_f<0x128>(hi));
-      if ((lane & 15) == a) G.rbox[(lane >> 4) * 8 + a] = lo;
-      if ((lane & 15) == 3 + a) G.rbox[(lane >> 4) * 8 + 3 + a] = hi;
+      const float lo = group_min(valid ? q3[a] : inf), hi = group_max(valid ? q3[a] : -inf);
+      if ((lane & (kCullLanes - 1)) == a) G.rbox[(lane / kCullLanes) * 8 + a] = lo;
+      if ((lane & (kCullLanes - 1)) == 3 + a) G.rbox[(lane / kCullLanes) * 8 + 3 + a] = hi;
     }
   }
 #endif
