@@ -342,8 +342,8 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
       lds_add(in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash, inc);
       s.c_hi += in ? 1u : 0u;
     }
-    if (true) return lane_in;
-#endif
+#else
+    (void)trash;
 #pragma unroll
     for (int t = 0; t < G; t++) {
       const uint32_t v = u[t];
@@ -358,6 +358,7 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
         s.c_hi++;
       }
     }
+#endif
   } else {
     const uint32_t bl = s.band_lo, bw = s.band_w;
     bool any = false;
