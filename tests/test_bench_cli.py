@@ -42,6 +42,7 @@ def test_bench_single_rank_cpu():
     assert rec["config"]["sampled_exact"] == "256/256"
     assert "(k=8) on 0.02M float3" in rec["metric"]
     assert rec["detail"]["phase_ms_max_over_ranks"]["knn_local"] > 0
+    assert rec["config"]["knn_kernels"] == ["cpu"]
 
 
 @pytest.mark.gpu
@@ -73,6 +74,7 @@ def test_bench_single_gpu_pipelined():
     assert rec["config"]["all_finite"] is True
     assert rec["config"]["sampled_exact"] == "512/512"
     assert "two different point sets" in rec["data"]
+    assert rec["config"]["knn_kernels"] == ["grid"]  # uniform points: the cell-grid kernel
 
 
 @pytest.mark.gpu
