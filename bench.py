@@ -86,10 +86,11 @@ def parse():
     ap.add_argument("--direct-out", type=int, default=-1,
                     help="1 = on one rank the k-NN kernel writes the distances straight into the "
                          "pinned host buffer over PCIe while it runs (no device-to-host copy after "
-                         "it); 0 = device buffer + copy; -1 (default) = a lone set: 1 when k >= 48 "
-                         "(where the PCIe writes hide under the kernel, "
-                         "pipelines.direct_host_out_pays); the stream of sets: 0 (the copy runs "
-                         "on a side stream under the next set)")
+                         "it); 0 = device buffer + one copy; -1 (default) = a lone set: the copy "
+                         "when the cell grid is built (its kernel outruns the PCIe writes), the "
+                         "direct writes for the bucket-tree kernel when k >= 48 "
+                         "(pipelines.query_into); the stream of sets: 0 (the copy runs on a side "
+                         "stream under the next set)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="1 = capture the whole single-rank step (H2D, index build, k-NN, results "
                          "to host) in one HIP graph after the warmup and replay it per step; "
@@ -185,15 +186,16 @@ def main():
     # (auto: from 1e7 points; below that one HIP-graph replay per set is cheaper than the
     # eager launches of the stream: 1e6 k=8 711 vs 702 Mpts/s, profiles/r2_s3_table)
     pipelined = (args.pipeline == 1 or (args.pipeline < 0 and n_total >= PIPELINE_MIN_POINTS)) \
-        and device.type == "cuda" \
-        and args.variant == "unordered" and args.mode == "halo"
+        and device.type == "cuda" and args.mode == "halo"
     host_sets = [make_points(n_total, rank, world, device, args.variant, d) for d in range(2 if pipelined else 1)]
     host_outs = [torch.empty(h.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda") for h in host_sets]
     host_pts, host_out = host_sets[0], host_outs[0]
 
     info_last = None
-    direct = (PL.direct_host_out_pays(args.k) if args.direct_out < 0 else bool(args.direct_out)) \
-        and not comm.distributed and device.type == "cuda"
+    # one GPU rank: the pinned output is passed down and pipelines.query_into picks direct
+    # PCIe writes or device buffer + copy (--direct-out forces one)
+    single_gpu = not comm.distributed and device.type == "cuda"
+    direct = None if args.direct_out < 0 else bool(args.direct_out)
 
     def step():
         with trace.range("lsknn:step"):
@@ -218,13 +220,14 @@ def main():
         elif args.mode == "peer":
             out = RA.peer_knn(pts, comm, cfg, info)
         elif args.variant == "unordered":
-            # one rank: the kernel writes host_out directly (k >= 48); several ranks: the
-            # grouped result return copies each group's rows into it under the exchange
+            # one rank: host_out through pipelines.query_into (device buffer + copy for the
+            # grid kernel); several ranks: the grouped result return copies each group's
+            # rows into it under the exchange
             out = PL.unordered_knn(pts, comm, cfg, info, n_total=n_total,
-                                   out=out_h if (direct or (comm.distributed and device.type == "cuda"))
-                                   else None)
+                                   out=out_h if device.type == "cuda" else None, direct=direct)
         else:
-            out = PL.prepartitioned_knn(pts, comm, cfg, info, out=out_h if direct else None)
+            out = PL.prepartitioned_knn(pts, comm, cfg, info, out=out_h if single_gpu else None,
+                                        direct=direct)
         if out.data_ptr() != out_h.data_ptr():
             out_h.copy_(out, non_blocking=True)
         info_last = info
@@ -261,8 +264,10 @@ def main():
         # k-NN; several ranks: set i's results to host under set i+1
         # the stream keeps results in device memory and copies them to host on a side
         # stream: the kernel's direct PCIe writes contend with the next set's upload (1B,
-        # k=100: 1319 vs 1373 ms per set); a lone set (single_set_ms) writes directly
-        runner = SetStream(comm, cfg, direct_out=bool(args.direct_out) if args.direct_out >= 0 else False)
+        # k=100: 1319 vs 1373 ms per set); prePartitioned sets take the same stream (one
+        # rank: the same single-rank pipeline; several: no redistribution)
+        runner = SetStream(comm, cfg, direct_out=bool(args.direct_out) if args.direct_out >= 0 else False,
+                           variant=args.variant)
 
         def run_steps(n):
             with trace.range("lsknn:steps"):
@@ -275,6 +280,8 @@ def main():
             step()
     comm.barrier()
     _sync(device)
+    E.reset_kernels_used()  # report the kernels of the timed steps only
+    E.deferred_heavy_cells(clear=True)
     ncoll0 = comm.collectives()
     calls0 = dict(getattr(comm, "calls", {}))
     t0 = time.perf_counter()
@@ -293,13 +300,14 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.allreduce_(t, "max")
     elapsed = float(t.item())
+    kernels_timed = E.kernels_used()  # (gate reads: after the clock)
 
     ms = elapsed / args.steps * 1e3
     value = n_total * args.steps / elapsed / 1e6
-    heavy_unrefined = False
+    heavy_unrefined = E.deferred_heavy_cells(clear=True)
     if graph is not None:
         E.verify_captured_failures(clear=True)  # raises if any replay overflowed a failure list
-        heavy_unrefined = E.captured_heavy_cells(clear=True)
+        heavy_unrefined = E.captured_heavy_cells(clear=True) or heavy_unrefined
     # the sets the timed steps wrote last (pipelined: both sets when K >= 2)
     written = sorted({(args.steps - 1 - j) % len(host_sets) for j in range(min(args.steps, len(host_sets)))})
     finite_t = torch.tensor([sum(0 if host_outs[d].numel() == 0 or bool(torch.isfinite(host_outs[d]).all()) else 1
@@ -309,7 +317,9 @@ def main():
 
     # ---- untimed: sampled brute-force check of the timed result, then one instrumented step
     check = None
-    if args.verify > 0 and args.variant == "unordered":
+    if args.verify > 0:
+        # (prePartitioned: rank r's file is the block [b, e) of global ids too — the check
+        # counts every sampled id's distances over all ranks' points)
         b, _ = block_range(n_total, rank, world)
         for d in written:
             c = verify.sampled_exact(comm, host_sets[d], host_outs[d], b, n_total, args.k, args.verify)
@@ -373,7 +383,7 @@ def main():
                 "hip_graph": graph is not None,
                 "pipelined": pipelined,
                 "heavy_cells_unrefined": heavy_unrefined,
-                "knn_kernels": sorted(E.KERNELS_USED),
+                "knn_kernels": kernels_timed,
                 "all_finite": finite,
                 "sampled_exact": (f"{check['exact']}/{check['samples']}" if check else None),
             },

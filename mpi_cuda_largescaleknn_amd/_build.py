@@ -166,9 +166,36 @@ def build_mpi(force: bool = False, verbose: bool = False) -> str | None:
     return MPI_LIB
 
 
+# Measured-and-rejected experiments that a test still exercises (not part of the product
+# library): scripts/micro/<name>.hip -> lib/exp/liblsknn_<name>.so
+MICRO_DIR = os.path.join(os.path.dirname(PKG_DIR), "scripts", "micro")
+MICRO_LIBS = ["screen_ab"]
+
+
+def micro_lib(name: str) -> str:
+    return os.path.join(LIB_DIR, "exp", f"liblsknn_{name}.so")
+
+
+def build_micro(force: bool = False, verbose: bool = False) -> list[str]:
+    out = []
+    for name in MICRO_LIBS:
+        src = os.path.join(MICRO_DIR, f"{name}.hip")
+        lib = micro_lib(name)
+        if os.path.exists(src) and (force or _stale(lib, [src] + _headers())):
+            os.makedirs(os.path.dirname(lib), exist_ok=True)
+            if verbose:
+                print(f"[build] {os.path.basename(lib)}")
+            tmp = lib + ".tmp"
+            _run([_hipcc(), *HIP_FLAGS, "-I", os.path.join(CSRC, "hip"), "-I", CSRC, "-shared", src, "-o", tmp])
+            os.replace(tmp, lib)
+        out.append(lib)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = False) -> tuple[str, str]:
     build_comm(force, verbose)
     build_mpi(force, verbose)
+    build_micro(force, verbose)
     return build_host(force, verbose), build_hip(force, verbose)
 
 

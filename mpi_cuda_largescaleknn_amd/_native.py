@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 5  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 6  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -85,6 +85,9 @@ class KnnArgs(C.Structure):
         ("fail_cap", i64),
         ("debug_fail_mod", C.c_int32),
         ("pad1", C.c_int32),
+        ("gate", vp),
+        ("gate_on", C.c_int32),
+        ("pad2", C.c_int32),
     ]
 
 
@@ -165,6 +168,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_knn_exact": ([C.POINTER(KnnArgs), vp, vp, i64, vp], i32),
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_knn_grid": ([C.POINTER(KnnArgs), C.POINTER(GridView), vp], i32),
+        "lsk_hip_grid_decide": ([vp, vp, i64, i32, C.c_float, i32, vp, vp], i32),
         "lsk_hip_grid_build": ([vp, vp, i64, vp, i32, vp, vp], i32),
         "lsk_hip_key_levels": ([vp, i64, vp, vp], i32),
         "lsk_hip_grid_sq": ([vp, i64, vp, vp], i32),
@@ -181,7 +185,6 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_refalgo_extract": ([vp, i64, i32, vp, vp], i32),
         "lsk_hip_count_below": ([vp, i64, vp, vp, i32, vp, vp], i32),
         "lsk_hip_segment_bounds": ([vp, vp, i64, i64, vp, vp, vp], i32),
-        "lsk_hip_screen_ab": ([vp, i64, vp, i32, i32, vp, vp, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

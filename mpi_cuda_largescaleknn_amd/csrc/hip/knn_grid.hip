@@ -54,43 +54,29 @@ using lsk::fbits;
 #endif
 constexpr int kWPB = LSK_GRID_WPB;
 constexpr int kThreads = kWPB * lsk::kWave;
-constexpr int kBins = 40;                 // 16-bit bins, two per LDS dword (as knn_rows)
-// LSK_GRID_PAIRHIST: lanes l and l+32 share a dword (low / high half) of each bin row, so
-// a lane's increment is a per-lane constant and every candidate adds without a branch
-// (values past the range go to a trash row, kBins); else (as knn_rows) bins 2j and 2j+1
-// of one lane share a dword.
-#ifndef LSK_GRID_PAIRHIST
-#define LSK_GRID_PAIRHIST 1
-#endif
-#if LSK_GRID_PAIRHIST
+constexpr int kBins = 40;                 // 16-bit bins
+// Lanes l and l+32 share a dword (low / high half) of each bin row, so a lane's increment
+// is a per-lane constant and every candidate adds without a branch (values past the range
+// go to a trash row, kBins).
 constexpr int kPool = (kBins + 1) * 32;   // dwords per wave: histogram + trash row, or collect pool
-#else
-constexpr int kPool = kBins / 2 * 64;     // dwords per wave: histogram, or collect pool
-#endif
-// LSK_GRID_ROWCULL: a grandchild is needed when it lies within the cull radius of one of
-// the wave's four 16-query ROWS (each with its own box and radius, kept in LDS) instead of
-// the whole wave's box and largest radius: the union of the rows' regions is smaller
-// (0.918x the evaluations at 1e8 uniform, k = 100; 4 gap tests per grandchild): 0.088 ->
-// 0.085 s, 1B stream 1005 Mpts/s (profiles/r3_rowcull). With the row boxes in SGPRs the
-// extra pressure put spill reloads into the candidate loop and it was slower (0.091 s).
-#ifndef LSK_GRID_ROWCULL
-#define LSK_GRID_ROWCULL 1
-#endif
-// (LSK_GRID_ROWCULL=2: eight groups of 8 queries instead of four rows of 16)
-constexpr int kCullGroups = LSK_GRID_ROWCULL == 2 ? 8 : 4;
+// Grandchild culling by ROWS: a grandchild is needed when it lies within the cull radius
+// of one of the wave's four 16-query rows (each with its own box and radius, kept in LDS)
+// instead of the whole wave's box and largest radius: the union of the rows' regions is
+// smaller (0.918x the evaluations at 1e8 uniform, k = 100; 4 gap tests per grandchild):
+// 0.088 -> 0.085 s, 1B stream 1005 Mpts/s (profiles/r3_rowcull). With the row boxes in
+// SGPRs the extra pressure put spill reloads into the candidate loop and it was slower
+// (0.091 s); eight groups of 8 queries cut 11.9 % of the evaluations but spent it on twice
+// the gap tests (0.086 s).
+constexpr int kCullGroups = 4;
 constexpr int kCullLanes = 64 / kCullGroups;
 
-// max / min inside each cull group (DPP: quads, then the half-row or the row); every lane
-// of a group ends with the group's value
+// max inside each 16-lane row (DPP: quads, then the row); every lane of a row ends with
+// the row's value
 __device__ __forceinline__ float group_max(float v) {
   v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false)));
   v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false)));
-  if (kCullGroups == 8) {
-    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false)));
-  } else {
-    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false)));
-    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)));
-  }
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)));
   return v;
 }
 __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
@@ -162,11 +148,7 @@ __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
 }
 
 __device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
-#if LSK_GRID_PAIRHIST
   return (pool[b * 32u + ((uint32_t)lane & 31u)] >> (((uint32_t)lane & 32u) >> 1)) & 0xffffu;
-#else
-  return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
-#endif
 }
 
 __device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *pool, int lane) {
@@ -202,16 +184,8 @@ __device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int l
 // equals c_hi iff no counter wrapped.
 __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *pool, int lane) {
   uint32_t sum = 0;
-#if LSK_GRID_PAIRHIST
 #pragma unroll
   for (int b = 0; b < kBins; b++) sum += b < s.bin_hi ? hist_read(pool, (uint32_t)b, lane) : 0u;
-#else
-#pragma unroll
-  for (int j = 0; j < kBins / 2; j++) {
-    const uint32_t w = pool[j * lsk::kWave + lane];
-    sum += (2 * j < s.bin_hi ? (w & 0xffffu) : 0u) + (2 * j + 1 < s.bin_hi ? (w >> 16) : 0u);
-  }
-#endif
   return sum == s.c_hi;
 }
 
@@ -302,11 +276,9 @@ struct GridCtx {
   float eps;               // absolute slack of cell boundaries and the cull radius
   uint32_t lc;             // cell level
   float wlx, wly, wlz, whx, why, whz;  // box of the wave's queries
-#if LSK_GRID_ROWCULL
   float *rbox;             // LDS, per row r: [8r..8r+5] box of its 16 queries (lo xyz, hi
                            // xyz), [8r+6] its squared cull radius (cull_r2); read per cell
                            // (in SGPRs they pushed spill reloads into the candidate loop)
-#endif
   uint32_t *pool;
   uint32_t trash;          // LDS byte address of this lane's trash-row counter (opaque)
   int lane;
@@ -364,33 +336,25 @@ __device__ __forceinline__ float inflate_r2(float b, float eps) {
 
 template <int MODE>
 __device__ __forceinline__ float cull_r2(const Lane &s, GridCtx &G) {
-#if LSK_GRID_ROWCULL
   // row maxima (DPP inside the 16-lane rows), each row's radius, the wave's = the largest
-  float v = group_max(lane_bound<MODE>(s));
-  float r2 = inflate_r2(v, G.eps);  // this lane's group's radius
+  const float v = group_max(lane_bound<MODE>(s));
+  const float r2 = inflate_r2(v, G.eps);  // this lane's row's radius
   if ((G.lane & (kCullLanes - 1)) == 0) G.rbox[(G.lane / kCullLanes) * 8 + 6] = r2;
-  if (kCullGroups == 8) r2 = fmaxf(r2, dpp_f<0x128>(r2));  // pairs of groups -> rows
   const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 0);
   const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 16);
   const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 32);
   const uint32_t d = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(r2), 48);
   return __uint_as_float(max(max(a, b), max(c, d)));
-#else
-  return inflate_r2(wave_max_nonneg(lane_bound<MODE>(s)), G.eps);
-#endif
 }
 
 template <int MODE>
 __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3,
                                         uint32_t *pool, int lane, uint32_t hist_trash) {
   if (MODE == MODE_HIST) {
-#ifndef LSK_GRID_NOSKIP
     const uint32_t um = min(min(u0, u1), min(u2, u3));
     if (!__ballot(um < s.hi_b)) return;
-#endif
-    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
+    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift;
     const uint32_t u[4] = {u0, u1, u2, u3};
-#if LSK_GRID_PAIRHIST
     // every slot adds, without a branch: a value below hi_b to its bin (< bin_hi), any
     // other (past the range, or a lane not histogramming: hi_b = 0) to the trash row kBins,
     // which nothing reads; the compare also counts c_hi. A 16-bit wrap (65536 adds to one
@@ -409,34 +373,6 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
       const uint32_t a = in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash;
       lds_add(a, inc);
       s.c_hi += in ? 1u : 0u;
-    }
-    (void)sh1;
-    return;
-#endif
-#ifdef LSK_GRID_BRANCHLESS
-    // every slot adds (0 when out of range): no exec-mask round trip per candidate
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const uint32_t v = u[t];
-      const bool in = v < hb;
-      const uint32_t w = __builtin_elementwise_sub_sat(min(v, hb - 1u), lb);
-      const uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
-      const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
-      atomicAdd(&pool[dw * lsk::kWave + lane], in ? __umul24(half, 0xffffu) + 1u : 0u);
-      s.c_hi += in ? 1u : 0u;
-    }
-    return;
-#endif
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const uint32_t v = u[t];
-      if (v < hb) {
-        const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
-        const uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
-        const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
-        atomicAdd(&pool[dw * lsk::kWave + lane], __umul24(half, 0xffffu) + 1u);
-        s.c_hi++;
-      }
     }
   } else {
     const uint32_t bl = s.band_lo, bw = s.band_w;
@@ -646,7 +582,6 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
   if (!nonempty) return;
   G.cells_n++;
   const uint32_t sh = 10u - (G.lc + 2u);
-#if LSK_GRID_ROWCULL
   (void)r2;
   const uint32_t last = (1023u >> sh);
   float lx, hx, ly, hy, lz, hz;
@@ -661,10 +596,6 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
     in_any = in_any || g2 <= b[6];
   }
   const uint64_t need = __ballot(ne && in_any);
-#else
-  const float g2 = cell_gap2(G, c.xyz & 1023u, (c.xyz >> 10) & 1023u, c.xyz >> 20, sh);
-  const uint64_t need = __ballot(ne && g2 <= r2);
-#endif
   if (!need) return;
   LSK_GT(tp0);
   process_cell_stream<MODE>(s, G, c, need, need | ~nonempty);
@@ -791,17 +722,14 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
 }
 
 __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
-#if LSK_GRID_ROWCULL
   __shared__ uint32_t lds[kWPB][kPool + 8 * kCullGroups];
-#else
-  __shared__ uint32_t lds[kWPB][kPool];
-#endif
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
   const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
   const uint64_t wave = (uint64_t)blk * kWPB + wid;
   const uint64_t ngroups = (uint64_t)((A.nq + 63) / 64);
   if (wave >= ngroups) return;
+  if (A.gate && *A.gate != A.gate_on) return;  // the device chose knn_rows
   const int64_t q0 = (int64_t)wave * lsk::kBucket;
   const int64_t qi = q0 + lane;
   const bool valid = qi < A.nq;
@@ -827,9 +755,7 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   G.lc = (uint32_t)V.level;
   G.pool = pool;
   G.lane = lane;
-#if LSK_GRID_ROWCULL
   G.rbox = (float *)(pool + kPool);
-#endif
   G.trash = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u + (uint32_t)kBins * 128u;
   asm volatile("" : "+v"(G.trash));
   G.k = k;
@@ -852,7 +778,6 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   G.why = lsk::wave_max(valid ? s.qy : -inf);
   G.wlz = lsk::wave_min(valid ? s.qz : inf);
   G.whz = lsk::wave_max(valid ? s.qz : -inf);
-#if LSK_GRID_ROWCULL
   {
     // per-row boxes (an empty row: +inf / -inf, never needs anything)
     const float q3[3] = {s.qx, s.qy, s.qz};
@@ -863,7 +788,6 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
       if ((lane & (kCullLanes - 1)) == 3 + a) G.rbox[(lane / kCullLanes) * 8 + 3 + a] = hi;
     }
   }
-#endif
 
   bool dup;
   float r_est2 = own_group_estimate(s, nvalid, k, dup);
@@ -879,12 +803,7 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
     const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
     if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
     const uint32_t mb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, max(1u, nvalid / 2u));
-#ifdef LSK_GRID_EST_MEDIAN
-    // one range for the whole wave (the cull radius follows the largest lane range)
-    if (ok && mb < lsk::kInfBits) r_est2 = bitsf(mb) * (float)LSK_GRID_EST_MEDIAN;
-#else
     if (ok && mb < lsk::kInfBits) r_est2 = sqrtf(r_est2 * bitsf(mb)) * kEstCalib;
-#endif
   }
   if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
     r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
@@ -1179,7 +1098,33 @@ __global__ __launch_bounds__(256) void grid_sq_kernel(const uint4 *__restrict__ 
   }
 }
 
+__global__ void grid_decide_kernel(const unsigned long long *__restrict__ counts,
+                                   const unsigned long long *__restrict__ sq, int64_t n, int32_t g, float crowd,
+                                   int32_t check, int32_t *__restrict__ gate) {
+  if (threadIdx.x != 0) return;
+  int32_t ok = 1;
+  if (check) {
+    // distinct cells of level l = counts[l] + 1 (adjacent sorted keys that differ)
+    const double dg = (double)counts[g] + 1.0, dg1 = g >= 2 ? (double)counts[g - 1] + 1.0 : 1.0;
+    const double mean = (double)n / dg;
+    const double seen = (double)sq[0] / (double)(n > 0 ? n : 1);
+    ok = (dg >= 6.0 * dg1 && mean >= 2.0 && mean <= 256.0 && seen <= (double)crowd * (mean + 1.0)) ? 1 : 0;
+  }
+  gate[0] = ok;
+}
+
 }  // namespace
+
+extern "C" int lsk_hip_grid_decide(const unsigned long long *counts, const unsigned long long *sq, int64_t n,
+                                   int32_t g, float crowd, int32_t check, int32_t *gate, void *stream) {
+  if (g < 2 || g > 10) {
+    lsk::set_last_error("grid_decide: grandchild level must be in [2, 10]");
+    return 1;
+  }
+  grid_decide_kernel<<<1, 64, 0, (hipStream_t)stream>>>(counts, sq, n, g, crowd, check, gate);
+  LSK_CHECK_LAUNCH("grid_decide");
+  return 0;
+}
 
 extern "C" int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorted_keys, int64_t n,
                                   const float *box, int32_t level, uint32_t *slots, void *stream) {

@@ -75,18 +75,11 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 // Measured on 1e8 uniform points, k=100.
 constexpr int kBins = LSK_ROWS_BINS;  // histogram bins (1/8 octave of d² each at kShift0)
 static_assert(kBins % 2 == 0 && kBins <= 64, "two 16-bit bins per dword, <= 32 dwords");
-// LSK_ROWS_PAIRHIST (default, as knn_grid.hip): lanes l and l+32 share a dword (low /
-// high half) of each bin row, so a lane's increment is a per-lane constant and every
-// candidate adds without a branch — in range to its bin, otherwise to a trash row (kBins)
-// that nothing reads; else bins 2j and 2j+1 of one lane share a dword (exec-masked adds).
-#ifndef LSK_ROWS_PAIRHIST
-#define LSK_ROWS_PAIRHIST 1
-#endif
-#if LSK_ROWS_PAIRHIST
+// As knn_grid.hip: lanes l and l+32 share a dword (low / high half) of each bin row, so a
+// lane's increment is a per-lane constant and every candidate adds without a branch — in
+// range to its bin, otherwise to a trash row (kBins) that nothing reads (mixed_scale 2e7
+// k=100 77.6 -> 85.8 Mpts/s over exec-masked adds, profiles/r3_rows_hist).
 constexpr int kPool = (kBins + 1) * 32;  // dwords per wave: histogram + trash row, or collect pool
-#else
-constexpr int kPool = kBins / 2 * 64;  // dwords per wave: histogram, or collect pool
-#endif
 // 16 bins (2 octaves of d²) above the estimate: with Hilbert-sorted groups fewer
 // overflow retries than 12 (1e8 uniform, k=100: 0.155 vs 0.159 s; 8: 0.179 s)
 // (with the blended estimate below: 12 bins = 1.5 octaves; 1e8 uniform, k=100: 8 bins
@@ -192,11 +185,7 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
 }
 
 __device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
-#if LSK_ROWS_PAIRHIST
   return (pool[b * 32u + ((uint32_t)lane & 31u)] >> (((uint32_t)lane & 32u) >> 1)) & 0xffffu;
-#else
-  return (pool[(b >> 1) * lsk::kWave + lane] >> ((b & 1u) << 4)) & 0xffffu;
-#endif
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -252,11 +241,7 @@ __device__ __forceinline__ bool hist_shrink(Lane &s, const uint32_t *pool, int l
   // box and candidate is culled), so k + duplicates of a point cost k candidates, not all
   // of them (and bin 0's 16-bit counter cannot overflow)
   if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
-#if LSK_CROWD_ABORT
   return top > (uint32_t)LSK_CROWD_ABORT * k && crowd_refinable(s);
-#else
-  return false;
-#endif
 }
 
 // Wave min / max of NON-NEGATIVE floats without LDS round trips: DPP
@@ -327,14 +312,12 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
     if (!__ballot(lane_in)) return false;
     // bin = sat(v - lo_b) >> shift (< 64 for every v < hi_b); bins 2j, 2j+1 share the
     // lane's dword j as two 16-bit counters
-    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift, sh1 = sh + 1u;
-#if LSK_ROWS_PAIRHIST
+    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift;
     // branch-free: a value below hi_b to its bin, any other to the lane's trash row
     // (`trash`, an opaque per-lane LDS address, so the select is between addresses); the
     // compare also counts c_hi. 6 VALU per candidate, no exec-mask round trip.
     const uint32_t inc = 1u << (((uint32_t)lane & 32u) >> 1);
     const uint32_t row0 = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u;
-    (void)sh1;
 #pragma unroll
     for (int t = 0; t < G; t++) {
       const uint32_t v = u[t];
@@ -342,23 +325,6 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
       lds_add(in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash, inc);
       s.c_hi += in ? 1u : 0u;
     }
-#else
-    (void)trash;
-#pragma unroll
-    for (int t = 0; t < G; t++) {
-      const uint32_t v = u[t];
-      const bool in = v < hb;
-      // exec-masked update: lanes out of range do not issue it, so the bin index needs
-      // no clamp (v < hi_b <= lo_b + kBins << shift) and the increment no select
-      if (in) {
-        const uint32_t w = __builtin_elementwise_sub_sat(v, lb);
-        const uint32_t dw = __builtin_amdgcn_ubfe(w, sh1, 5u);
-        const uint32_t half = __builtin_amdgcn_ubfe(w, sh, 1u);
-        atomicAdd(&pool[dw * lsk::kWave + lane], __umul24(half, 0xffffu) + 1u);
-        s.c_hi++;
-      }
-    }
-#endif
   } else {
     const uint32_t bl = s.band_lo, bw = s.band_w;
     bool any = false;
@@ -412,7 +378,7 @@ struct WaveCtx {
   WaveLds *L;
   uint32_t *rl;
   uint32_t rcap;
-  uint32_t trash;  // LDS byte address of this lane's trash-row counter (opaque; PAIRHIST)
+  uint32_t trash;  // LDS byte address of this lane's trash-row counter (opaque)
   int lane, row;
   uint32_t k;
   uint32_t g;
@@ -1059,14 +1025,7 @@ constexpr uint32_t kNaNBits = 0x7fc00000u;
 __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *pool, int lane) {
   uint32_t sum = 0;
 #pragma unroll
-#if LSK_ROWS_PAIRHIST
   for (int b = 0; b < kBins; b++) sum += b < s.bin_hi ? hist_read(pool, (uint32_t)b, lane) : 0u;
-#else
-  for (int j = 0; j < kBins / 2; j++) {
-    const uint32_t w = pool[j * lsk::kWave + lane];
-    sum += (2 * j < s.bin_hi ? (w & 0xffffu) : 0u) + (2 * j + 1 < s.bin_hi ? (w >> 16) : 0u);
-  }
-#endif
   return sum == s.c_hi;
 }
 
@@ -1080,6 +1039,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid;
   const uint64_t ngroups = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
   if (wave >= ngroups) return;
+  if (A.gate && *A.gate != A.gate_on) return;  // the device chose the grid kernel
   const uint32_t g = lsk::uniform(A.groups ? A.groups[wave] : (uint32_t)wave);
   const int64_t q0 = (int64_t)g * lsk::kBucket;
   const int64_t qi = q0 + lane;

@@ -125,6 +125,9 @@ typedef struct lsk_knn_args {
   int64_t fail_cap;         // (the count may exceed the capacity: then the host reruns all)
   int32_t debug_fail_mod;   // tests only: also fail every query qi with qi % mod == 0
   int32_t pad1;
+  const int32_t *gate;      // optional device flag (lsk_hip_grid_decide): the rows / grid
+  int32_t gate_on;          // kernel runs only when *gate == gate_on (else every wave
+  int32_t pad2;             // returns at once): both are queued, the device picks one
 } lsk_knn_args;
 
 // Production kernel: 4 x 16-query rows, 16-bit LDS histogram radix select. Queries it
@@ -159,6 +162,13 @@ int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorted_keys, int
 int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream);
 // out[0] = sum over slots of population^2 (zeroed here).
 int lsk_hip_grid_sq(const uint32_t *slots, int64_t nslot, unsigned long long *out, void *stream);
+// Device-side "does the grid apply" (no host read, graph-capturable): gate[0] = 1 iff the
+// level census (counts: lsk_hip_key_levels) says near-uniform 3-D data at grandchild level
+// g — occupied cells multiply by >= 6 from g-1 to g and their mean population is in
+// [2, 256] — and the mean population of a point's own grandchild (sq: lsk_hip_grid_sq /
+// n) is at most crowd * (mean + 1); check == 0: gate[0] = 1 unconditionally.
+int lsk_hip_grid_decide(const unsigned long long *counts, const unsigned long long *sq, int64_t n, int32_t g,
+                        float crowd, int32_t check, int32_t *gate, void *stream);
 // Near-uniform fast path of lsk_hip_knn_rows (same contract, same failure list): one tree
 // whose points are the queries, no groups / init_d2; candidates from the grid.
 int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *stream);
@@ -212,12 +222,6 @@ int lsk_hip_refalgo_extract(const unsigned long long *heaps, int64_t nq, int k, 
 // over the n points (nq <= 1024 queries; counts zeroed by the caller, accumulated).
 int lsk_hip_count_below(const float *pts, int64_t n, const float *q, const float *thr, int nq,
                         unsigned long long *counts, void *stream);
-
-// ---- MFMA vs VALU screening A/B (screen_ab.hip) -------------------------------------------
-// n curve-ordered points (n % 64 == 0) are also the queries; out[q] = kept pairs per lane;
-// mode 0 VALU canonical, 1 MFMA screen, 2 MFMA screen + viol += pairs wrongly dropped.
-int lsk_hip_screen_ab(const float *pts, int64_t n, const float *thr, int steps, int mode, uint32_t *out,
-                      uint32_t *viol, void *stream);
 
 #ifdef __cplusplus
 }

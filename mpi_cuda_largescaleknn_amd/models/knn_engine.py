@@ -76,11 +76,17 @@ class GridIndex:
     level: int               # cell level (grandchildren at level + 2)
     box: torch.Tensor        # the cube of the sort keys (device)
     inf4: torch.Tensor | None = None  # 4 x +inf on the device (candidate padding)
+    gate: torch.Tensor | None = None  # device int32 [1]: 1 = the grid applies (decided on
+                                      # the device, GRID=auto), None = always (GRID=on)
 
     def view(self) -> tuple:
         if self.inf4 is None:
             self.inf4 = torch.full((4,), math.inf, dtype=torch.float32, device=self.slots.device)
-        return (self.slots, self.level, self.box, self.inf4)
+        return (self.slots, self.level, self.box, self.inf4, self.gate)
+
+    def applies(self) -> bool:
+        """Host read of the device decision (reporting only; never on the hot path)."""
+        return self.gate is None or bool(int(self.gate.item()))
 
 
 @dataclass
@@ -124,11 +130,16 @@ class KnnStats:
 
 
 def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
-                keys: tuple | None = None, grid: bool = False) -> LocalIndex:
+                keys: tuple | None = None, grid: bool = False, density_n: int | None = None,
+                grid_level: int | None = None) -> LocalIndex:
     """Sort points along the space-filling curve of `box` (default: their own bounds) and
     build the bucket tree. `keys` = (keys, iota) computed already (the streamed upload
     keys each chunk as it lands). `grid`: also index the sorted points by the cell grid of
-    the fast local k-NN pass (build_grid; GPU, outside graph captures)."""
+    the fast local k-NN pass (build_grid, GPU). `density_n`: the number of points that
+    fill `box` (a rank's share of a global box: the global count; default: n).
+    `grid_level` (tests): force the grid's grandchild level.
+    No host read on the way unless an over-full key cell needs the eager refinement
+    (refine_heavy_cells; under host_sync_free() not even that)."""
     points = points.contiguous()
     n = points.shape[0]
     if box is None:
@@ -140,8 +151,29 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     nodes, qnodes, depth = K.build_tree(pts, n)
     index = LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
     if grid:
-        index.grid = build_grid(index, skeys)
+        index.grid = build_grid(index, skeys, density_n, grid_level)
     return index
+
+
+def grid_level_for(density_n: int, n_local: int, ms: float = GRID_MS) -> int:
+    """Grandchild level of the grid from point counts alone (no census, no host read):
+    the level whose occupied cells would hold closest to `ms` points on average, in log
+    scale, for `density_n` uniform points filling the cube (mean population of the
+    occupied cells = lam / (1 - e^-lam), lam = density_n / 8^g; 1B -> 9, 1e8 -> 8,
+    1e7 -> 7 — what the census picks for uniform data), then capped so that the slot
+    table (16 KiB... 1 KiB per level g-2 cell) stays within 48 B per local point + 64 MiB:
+    a rank's share of a large global cube does not allocate the whole cube's finest table
+    (a capped level is coarser, hence slower, never wrong)."""
+    best, err = 2, math.inf
+    for g in range(2, 11):
+        lam = max(density_n, 1) / float(8 ** g)
+        mean = lam / -math.expm1(-lam) if lam > 1e-12 else 1.0
+        e = abs(math.log(max(mean, 1e-9) / ms))
+        if e < err:
+            best, err = g, e
+    while best > 2 and 1024 * 8 ** (best - 2) > 48 * max(n_local, 1) + (64 << 20):
+        best -= 1
+    return best
 
 
 def grid_level(distinct: list[int], n: int, ms: float = GRID_MS) -> int:
@@ -169,25 +201,27 @@ def grid_applies(distinct: list[int], n: int, g: int) -> bool:
     return distinct[g] >= 6 * distinct[g - 1] and 2.0 <= mean <= 256.0
 
 
-def build_grid(index: LocalIndex, skeys: torch.Tensor) -> GridIndex | None:
-    """Cell grid over index's sorted points (knn_grid.hip), or None when it does not apply
-    (CPU, graph capture, GRID=off, or crowded sub-cells under GRID=auto: clustered or
-    multi-scale data keeps the bucket-tree walk of knn_rows, which adapts to density).
-    Two host reads (the level census and the crowding sum)."""
+def build_grid(index: LocalIndex, skeys: torch.Tensor, density_n: int | None = None,
+               level: int | None = None) -> GridIndex | None:
+    """Cell grid over index's sorted points (knn_grid.hip), or None (CPU, GRID=off).
+
+    The level comes from the point counts (grid_level_for); whether the grid applies is
+    decided ON THE DEVICE (GRID=auto: lsk_hip_grid_decide from the level census and the
+    crowding sum — clustered or multi-scale data keeps the bucket-tree walk of knn_rows,
+    which adapts to density): the k-NN launch queues both kernels and the device runs the
+    chosen one. No host read, so the build is graph-capturable and a stream of sets never
+    waits for the previous set's k-NN here."""
     n = index.n
-    if GRID == "off" or n == 0 or not K.is_gpu(index.pts) or torch.cuda.is_current_stream_capturing():
+    if GRID == "off" or n == 0 or not K.is_gpu(index.pts):
         return None
-    distinct = K.key_levels(skeys[:n])
-    g = grid_level(distinct, n)
-    if GRID == "auto" and not grid_applies(distinct, n, g):
-        return None
+    g = level if level is not None else grid_level_for(density_n if density_n is not None else n, n)
     slots = K.grid_build(index.pts, skeys, n, index.box, g - 2)
+    gate = None
     if GRID == "auto":
-        seen = K.grid_sq(slots) / n          # mean population of a point's own grandchild
-        mean = n / max(1, distinct[g])
-        if seen > GRID_CROWD * (mean + 1.0):
-            return None
-    return GridIndex(slots, g - 2, index.box)
+        counts = K.key_levels_dev(skeys[:n])
+        sq = K.grid_sq_dev(slots)
+        gate = K.grid_decide(counts, sq, n, g, GRID_CROWD, True)
+    return GridIndex(slots, g - 2, index.box, gate=gate)
 
 
 HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key
@@ -199,6 +233,31 @@ HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-l
 REFINE_CAPTURE = False
 LAST_REFINED = False
 CAPTURED_HEAVY: list = []
+# Under host_sync_free() (a stream of point sets) the eager over-full-cell check does not
+# read its flag either: it is kept here like a captured one (results stay exact, an
+# unrefined cell only costs speed) and the stream reports it once the sets are done.
+_SYNC_FREE = [0]
+DEFERRED_HEAVY: list = []
+
+
+class host_sync_free:
+    """Context: index builds queue no host read (see DEFERRED_HEAVY)."""
+
+    def __enter__(self):
+        _SYNC_FREE[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _SYNC_FREE[0] -= 1
+        return False
+
+
+def deferred_heavy_cells(clear: bool = False) -> bool:
+    """Whether a build under host_sync_free() met an over-full cell it did not refine."""
+    hit = any(bool(f) for f in DEFERRED_HEAVY)
+    if clear:
+        DEFERRED_HEAVY.clear()
+    return hit
 
 
 def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
@@ -221,6 +280,10 @@ def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Te
         if REFINE_CAPTURE:
             return _refine_all_cells(points, skeys, perm)
         CAPTURED_HEAVY.append(heavy_any)
+        return perm
+    if _SYNC_FREE[0] and K.is_gpu(skeys):
+        DEFERRED_HEAVY.append(heavy_any)
+        del DEFERRED_HEAVY[:-1024]
         return perm
     if not bool(heavy_any):
         return perm
@@ -382,7 +445,11 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     use_grid = (impl == "rows" and index.grid is not None and len(trees) == 1 and groups is None
                 and init_d2 is None and cfg.k <= K.ROWS_MAX_K)
     if groups is None:  # (a whole-set pass, not a halo re-query)
-        KERNELS_USED.add("grid" if use_grid else impl)
+        if use_grid and index.grid.gate is not None:
+            GATES_SEEN.append(index.grid.gate)  # grid or rows: resolved by kernels_used()
+            del GATES_SEEN[:-1024]  # (reporting only: a long stream keeps the last sets)
+        else:
+            KERNELS_USED.add("grid" if use_grid else impl)
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
                    grid=index.grid.view() if use_grid else None, **kw)
@@ -418,8 +485,22 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
 
 
 # k-NN kernels the whole-set passes of this process used ("grid", "rows", "exact"): the
-# bench reports them next to its number
+# bench reports them next to its number. Passes whose kernel the device picks leave their
+# gate in GATES_SEEN; kernels_used() reads them (a host read: after the timed region).
 KERNELS_USED: set = set()
+GATES_SEEN: list = []
+
+
+def kernels_used() -> list:
+    used = set(KERNELS_USED)
+    for gate in GATES_SEEN:
+        used.add("grid" if int(gate.item()) else "rows")
+    return sorted(used)
+
+
+def reset_kernels_used() -> None:
+    KERNELS_USED.clear()
+    GATES_SEEN.clear()
 
 
 def settle(deferred: list) -> bool:

@@ -240,10 +240,15 @@ def radius_hint(box: torch.Tensor, n_total: int, k: int) -> torch.Tensor:
 ROWS_MAX_K = 65535  # 16-bit histogram bins of knn_rows; larger k go to the exact kernel
 
 
+FAIL_CAP_OVERRIDE: int | None = None  # tests: force failure-list overflows (whole reruns)
+
+
 def fail_capacity(work: int) -> int:
     """Capacity of the failure list of one knn_rows launch over `work` queries: all of
     them up to 64M, then 1/16 of them (a failure count above it makes the host rerun the
     whole query on the exact kernel, see knn_engine.query)."""
+    if FAIL_CAP_OVERRIDE is not None:
+        return max(1, min(work, FAIL_CAP_OVERRIDE))
     return max(1, min(work, max(1 << 26, work >> 4)))
 
 
@@ -301,9 +306,10 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     out_perm / out_final (optional, fused scatter): the kernels also write
     out_final[out_perm[q]] = final distance; out_d2 may then be None.
     debug_fail_mod (tests): the rows kernel also fails every query q with q % mod == 0.
-    grid (impl "grid"): (slots, level, box, inf4) of knn_engine.GridIndex — the cell-grid
-    candidate source of knn_grid.hip for one tree whose points are the queries (same
-    failure list and backstop as "rows").
+    grid (impl "grid"): (slots, level, box, inf4[, gate]) of knn_engine.GridIndex — the
+    cell-grid candidate source of knn_grid.hip for one tree whose points are the queries
+    (same failure list and backstop as "rows"); with a device gate (int32 [1]) the grid
+    kernel runs iff gate == 1 and knn_rows iff gate == 0.
     Returns the launch's FailWord.
     """
     if (out_perm is None) != (out_final is None):
@@ -353,9 +359,19 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_count = _ptr(count)
     a.fail_cap = cap
     if impl == "grid":
-        slots, level, gbox, inf4 = grid
+        slots, level, gbox, inf4 = grid[:4]
+        gate = grid[4] if len(grid) > 4 else None
         gv = GridView(_ptr(slots), None, _ptr(gbox), _ptr(inf4), int(level), 0)
+        if gate is not None:
+            # the device decides (lsk_hip_grid_decide): both kernels are queued, the one
+            # not chosen returns at its first instruction (no host read, graph-capturable)
+            a.gate = _ptr(gate)
+            a.gate_on = 1
         check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
+        if gate is not None:
+            a.gate_on = 0
+            check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
+        a.gate = None
     else:
         check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
     # exact backstop over the failure list (device-side count: empty list = short no-op)
@@ -385,6 +401,31 @@ def grid_build(sorted_pts: torch.Tensor, sorted_keys: torch.Tensor, n: int, box:
     check(_native.hip().lsk_hip_grid_build(_ptr(sorted_pts), _ptr(sorted_keys), n, _ptr(box), level, _ptr(slots),
                                            _stream(sorted_pts)), "grid_build")
     return slots
+
+
+def key_levels_dev(skeys: torch.Tensor) -> torch.Tensor:
+    """key_levels without the host read: int64 [11] on the device, counts[l] = distinct
+    level-l cells - 1 (the raw lsk_hip_key_levels output)."""
+    cnt = torch.zeros(11, dtype=torch.int64, device=skeys.device)
+    if skeys.shape[0] > 0:
+        check(_native.hip().lsk_hip_key_levels(_ptr(skeys), skeys.shape[0], _ptr(cnt), _stream(skeys)),
+              "key_levels")
+    return cnt
+
+
+def grid_sq_dev(slots: torch.Tensor) -> torch.Tensor:
+    """grid_sq without the host read: int64 [1] on the device."""
+    out = torch.empty(1, dtype=torch.int64, device=slots.device)
+    check(_native.hip().lsk_hip_grid_sq(_ptr(slots), slots.shape[0], _ptr(out), _stream(slots)), "grid_sq")
+    return out
+
+
+def grid_decide(counts: torch.Tensor, sq: torch.Tensor, n: int, g: int, crowd: float, check_uniform: bool):
+    """Device flag int32 [1]: 1 iff the grid applies (lsk_hip_grid_decide), no host read."""
+    gate = torch.empty(1, dtype=torch.int32, device=counts.device)
+    check(_native.hip().lsk_hip_grid_decide(_ptr(counts), _ptr(sq), n, g, C.c_float(crowd), int(check_uniform),
+                                            _ptr(gate), _stream(counts)), "grid_decide")
+    return gate
 
 
 def grid_sq(slots: torch.Tensor) -> int:

@@ -530,7 +530,20 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
     stream it returns."""
     stats = info.stats if cfg.collect_stats else None
     gpu = K.is_gpu(index.pts)
-    if not OVERLAP_HALO or (gpu and torch.cuda.is_current_stream_capturing()):
+    capturing = gpu and torch.cuda.is_current_stream_capturing()
+    if comm.size == 1 and not HALO_ONE_RANK:
+        # one rank (a forced multi-rank run): no peer, so no halo — the local pass is the
+        # result; the hook's work is issued right behind the k-NN launch, the failure
+        # check after it
+        pend: list = []
+        d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True,
+                     deferred=None if capturing or not gpu else pend)
+        if hook is not None:
+            hook(torch.cuda.current_stream(index.device) if gpu else None)
+        E.settle(pend)
+        info.timer.mark("knn_local")
+        return d2
+    if not OVERLAP_HALO or capturing:
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
         info.timer.mark("knn_local")
         return halo_refine(index, d2, comm, cfg, hint2, info, final_out=final_out)
@@ -599,6 +612,11 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
     return out
 
 
+
+# A 1-rank group (forced multi-rank runs) has no peer, hence no halo: knn_with_halo skips
+# the publish / filter / exchange / re-query. True: run them anyway (the RCCL call-site
+# tests exercise the halo collectives on one GPU with it).
+HALO_ONE_RANK = os.environ.get("LSKNN_HALO_ONE_RANK", "0") == "1"
 
 # tests: streamed redistribution also for device-resident input (env LSKNN_FORCE_STREAM=1)
 FORCE_STREAM = os.environ.get("LSKNN_FORCE_STREAM", "0") == "1"
@@ -692,38 +710,57 @@ def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int
     return index, hint2
 
 
+def query_into(index: E.LocalIndex, hint2, cfg: E.KnnConfig, info: RunInfo, out: torch.Tensor,
+               direct: bool | None = None, deferred: list | None = None) -> torch.Tensor:
+    """The k-NN kernel writes the final distances in input order (fused scatter). `out`
+    in pinned host memory: direct=True — the kernel writes it over PCIe while it runs;
+    False — a device buffer, then one 4 B/point copy (returned is `out` either way);
+    None — False when the index has a cell grid (the grid kernel outruns the random 4-byte
+    PCIe writes: 1B uniform, k=100, 1321 ms direct vs ~950 ms for the kernel alone), for a
+    deferred failure check (the caller copies after it) and below k = 48 (the bucket-tree
+    kernel hides the writes only from there: direct_host_out_pays), else True."""
+    stats = info.stats if cfg.collect_stats else None
+    host = out.device.type == "cpu" and index.pts.device.type == "cuda"
+    if host and direct is None:
+        direct = index.grid is None and deferred is None and direct_host_out_pays(cfg.k)
+    if host and not direct:
+        dev_out = torch.empty(index.n, dtype=torch.float32, device=index.device)
+        E.query(index, cfg, hint2, stats=stats, final_out=dev_out, deferred=deferred)
+        if deferred is not None:
+            return dev_out  # the caller copies it once the failure check has run
+        out.copy_(dev_out, non_blocking=True)
+        return out
+    E.query(index, cfg, hint2, stats=stats, final_out=out, deferred=deferred)
+    return out
+
+
 def local_query(index: E.LocalIndex, hint2, cfg: E.KnnConfig, info: RunInfo | None = None,
-                out: torch.Tensor | None = None, deferred: list | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, deferred: list | None = None,
+                direct: bool | None = None) -> torch.Tensor:
     """Single-rank second half: the k-NN kernel writes the final distances in input order
-    (fused scatter) into `out` (see unordered_knn). `deferred`: as in knn_engine.query."""
+    (fused scatter) into `out` (see unordered_knn; direct: query_into). `deferred`: as in
+    knn_engine.query; a pinned host `out` then comes back as a device result unless
+    direct=True (SetStream copies it after the check)."""
     info = info or RunInfo(PhaseTimer(False, index.device))
     out = _check_out(out, index.n, index.pts)
-    host = out.device.type == "cpu" and index.pts.device.type == "cuda"
-    if host and index.grid is not None and deferred is None:
-        # the cell-grid kernel outruns the random 4-byte PCIe writes of a direct output
-        # (1B uniform, k=100: 1321 ms direct vs ~950 ms for the kernel alone): write the
-        # device and copy the 4 B/point back in one transfer
-        dev_out = torch.empty(index.n, dtype=torch.float32, device=index.device)
-        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=dev_out)
-        out.copy_(dev_out, non_blocking=True)
-    else:
-        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out,
-                deferred=deferred)
+    out = query_into(index, hint2, cfg, info, out, direct=direct, deferred=deferred)
     info.timer.mark("knn_local")
     return out
 
 
 def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
-                  n_total: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+                  n_total: int | None = None, out: torch.Tensor | None = None,
+                  direct: bool | None = None) -> torch.Tensor:
     """k-th-NN distance of every local point (input order) for a globally unordered set
     block-partitioned over ranks (reference unorderedData variant).
 
     `points` may live in (pinned) host memory: on several ranks the redistribution then
     streams them to the device in chunks overlapped with the exchange
     (redistribute_stream); on one rank they are copied first.
-    `out` (optional, float32 [n_local]): where the distances go. On one rank the k-NN
-    kernel writes them there directly — a pinned host tensor receives them straight over
-    PCIe while the kernel runs (no device-to-host copy afterwards)."""
+    `out` (optional, float32 [n_local]): where the distances go. On one rank a pinned host
+    `out` is written by the k-NN kernel over PCIe while it runs, or through a device buffer
+    and one copy (`direct`, see query_into: by default the copy when the cell grid is
+    built, the direct writes for the bucket-tree kernel)."""
     info = info or RunInfo(PhaseTimer(False, comm.device))
     info.timer.start()
     points = points.contiguous()
@@ -736,7 +773,7 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     dev = comm.device
     if not comm.distributed:
         index, hint2 = local_build(points, comm, cfg, n_total, info)
-        return local_query(index, hint2, cfg, info, out)
+        return local_query(index, hint2, cfg, info, out, direct=direct)
     if not streamed:
         return compute_set(redistribute_set(points, comm, cfg, n_total, info), comm, cfg, info, out=out)
     R = redistribute_stream(points, comm, info)
@@ -853,7 +890,7 @@ IMBALANCE_LIMIT = 1.2  # --balance auto: rebalance when max/mean points per rank
 
 def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
                        info: RunInfo | None = None, out: torch.Tensor | None = None,
-                       balance: str = "auto") -> torch.Tensor:
+                       balance: str = "auto", direct: bool | None = None) -> torch.Tensor:
     """k-th-NN distance of every local point (input order) when each rank holds one
     (spatially coherent) input file (reference prePartitionedData variant). `out` as in
     unordered_knn (on one rank a pinned host tensor is written by the kernel directly).
@@ -889,7 +926,7 @@ def prepartitioned_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig,
     info.timer.mark("build")
     if not comm.distributed:  # fused scatter: final distances straight from the k-NN kernel
         out = _check_out(out, n_local, points)
-        E.query(index, cfg, hint2, stats=info.stats if cfg.collect_stats else None, final_out=out)
+        out = query_into(index, hint2, cfg, info, out, direct=direct)
         info.timer.mark("knn_local")
         return out
     res = torch.empty(n_local, dtype=torch.float32, device=points.device)

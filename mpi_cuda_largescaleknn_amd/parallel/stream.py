@@ -15,7 +15,9 @@ before ~1.4 s of index build and k-NN. `SetStream` overlaps them across sets:
   is queued, so it runs under set i's k-NN (pipelines.compute_set hook; set i's halo
   exchange and result return are ordered after its collectives, one communicator never
   has two collectives in flight); set i's returned distances go device -> host on a
-  third stream under set i+1 (kept alive with record_stream).
+  third stream, queued from set i+1's hook so the copy runs under set i+1's k-NN (kept
+  alive with record_stream). No host sync between sets (events order the input-buffer
+  reuse), and no host read inside an index build (knn_engine.host_sync_free).
 
 Every set is still uploaded, redistributed (several ranks), built, queried and returned in
 full; only the order in which independent work is issued changes. On a CPU device the sets
@@ -55,13 +57,20 @@ class SetStream:
     neighbouring sets overlapped (see module doc).
 
     comm / cfg: as for pipelines.unordered_knn. direct_out (one rank): the kernel writes
-    the distances into the pinned host outputs itself (pipelines.direct_host_out_pays).
+    the distances into the pinned host outputs itself (pipelines.query_into).
+    variant: "unordered" (block-partitioned sets, spatially redistributed on several
+    ranks) or "prepartitioned" (each rank's set is its own file: on one rank the same
+    pipeline; on several, pipelines.prepartitioned_knn per set with the uploads and result
+    copies overlapped).
     """
 
     def __init__(self, comm: Comm, cfg: E.KnnConfig, direct_out: bool = True,
-                 build_ahead: bool | None = None):
+                 build_ahead: bool | None = None, variant: str = "unordered"):
+        if variant not in ("unordered", "prepartitioned"):
+            raise ValueError(f"SetStream: variant must be unordered or prepartitioned, not {variant!r}")
         self.comm = comm
         self.cfg = cfg
+        self.variant = variant
         self.device = comm.device
         self.gpu = self.device.type == "cuda"
         self.direct_out = bool(direct_out) and not comm.distributed
@@ -110,18 +119,27 @@ class SetStream:
         n_totals = list(n_totals) if n_totals is not None else [None] * n
         new_info = info_factory or (lambda: PL.RunInfo(PL.PhaseTimer(False, self.device)))
         done = on_done or (lambda i: None)
-        if not self.gpu:
-            for i in range(n):
-                info = new_info()
+        if self.gpu:
+            with E.host_sync_free():  # no host read inside a build (knn_engine.build_index)
+                if self.comm.distributed and self.variant == "prepartitioned":
+                    return self._run_prepartitioned(inputs, outputs, new_info, done)
+                if self.comm.distributed:
+                    return self._run_distributed(inputs, outputs, n_totals, new_info, done)
+                if self.build_ahead:  # (one rank)
+                    return self._run_build_ahead(inputs, outputs, n_totals, new_info, done)
+                return self._run_local(inputs, outputs, n_totals, new_info, done)
+        for i in range(n):  # CPU: one set after the other
+            info = new_info()
+            if self.variant == "prepartitioned":
+                out = PL.prepartitioned_knn(inputs[i], self.comm, self.cfg, info)
+            else:
                 out = PL.unordered_knn(inputs[i], self.comm, self.cfg, info, n_total=n_totals[i])
-                outputs[i].copy_(out)
-                self.last_info = info
-                done(i)
-            return
-        if self.comm.distributed:
-            return self._run_distributed(inputs, outputs, n_totals, new_info, done)
-        if self.build_ahead:  # (one rank)
-            return self._run_build_ahead(inputs, outputs, n_totals, new_info, done)
+            outputs[i].copy_(out)
+            self.last_info = info
+            done(i)
+
+    def _run_local(self, inputs, outputs, n_totals, new_info, done) -> None:
+        n = len(inputs)
         cur = torch.cuda.current_stream(self.device)
         if n:
             self._prefetch(0, inputs[0])
@@ -157,7 +175,7 @@ class SetStream:
         cur = torch.cuda.current_stream(self.device)
         pend: list = []
         res = PL.local_query(index, hint2, self.cfg, info, outputs[i] if self.direct_out else None,
-                             deferred=pend)
+                             deferred=pend, direct=True if self.direct_out else None)
         ev = torch.cuda.Event()
         ev.record(cur)
         return (i, None if res.data_ptr() == outputs[i].data_ptr() else res, ev, pend)
@@ -254,7 +272,56 @@ class SetStream:
         with torch.cuda.stream(self.copy_stream):
             self._buffer(j % 2, host).copy_(host, non_blocking=True)
 
+    def _run_prepartitioned(self, inputs, outputs, new_info, done) -> None:
+        """Several ranks, one file per rank and set: set i+1's upload runs under set i
+        (copy stream), set i's result copy under set i+1 (output stream, queued once set
+        i+1's work is), no host sync between sets beyond the collectives' own."""
+        n = len(inputs)
+        cur = torch.cuda.current_stream(self.device)
+        if n == 0:
+            return
+        self._prefetch(0, inputs[0])
+        copies: list = []
+        prev = None
+        for i in range(n):
+            cur.wait_stream(self.copy_stream)  # set i's points are on the device
+            pts = self._dbuf[i % 2]
+            if i + 1 < n:
+                self._prefetch(i + 1, inputs[i + 1])  # after set i-1's reads of that buffer
+            info = new_info()
+            with trace.range(f"lsknn:set {i}"):
+                res = PL.prepartitioned_knn(pts, self.comm, self.cfg, info)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            if prev is not None:
+                j, r, e = prev
+                self.out_stream.wait_event(e)
+                with torch.cuda.stream(self.out_stream):
+                    outputs[j].copy_(r, non_blocking=True)
+                    ce = torch.cuda.Event()
+                    ce.record(self.out_stream)
+                r.record_stream(self.out_stream)
+                copies.append((j, ce))
+            prev = (i, res, ev)
+            del res
+            self.last_info = info
+            while copies and copies[0][1].query():
+                done(copies.pop(0)[0])
+        j, r, e = prev
+        with torch.cuda.stream(self.out_stream):
+            self.out_stream.wait_event(e)
+            outputs[j].copy_(r, non_blocking=True)
+        self.out_stream.synchronize()
+        for j, _ in copies:
+            done(j)
+        done(n - 1)
+
     def _run_distributed(self, inputs, outputs, n_totals, new_info, done) -> None:
+        """Several ranks. Set i+1's redistribution runs under set i's k-NN (the compute_set
+        hook), and set i-1's result goes to host memory on the output stream from the same
+        hook, i.e. under set i's k-NN too (queued earlier, its PCIe writes slowed set i's
+        index build). No host sync between sets: events order the buffer reuse, and the
+        host only waits where a collective's sizes are needed."""
         comm, cfg, dev = self.comm, self.cfg, self.device
         cur = torch.cuda.current_stream(dev)
         redist = self.redist_stream
@@ -267,23 +334,46 @@ class SetStream:
                 n_totals[j] = int(t.item())
         if n == 0:
             return
-        fin: list = []
+        red_ev: list = [None, None]  # event after the redistribution that read input buffer b
         self._prefetch(0, inputs[0])
         cur.wait_stream(self.copy_stream)
         P = PL.redistribute_set(self._dbuf[0], comm, cfg, n_totals[0], new_info())
+        red_ev[0] = torch.cuda.Event()
+        red_ev[0].record(cur)
         if n > 1:
             self._prefetch(1, inputs[1])
+        pending: list = []  # [(j, device result, event after it)] not yet copied to host
+        copies: list = []   # [(j, event after its copy to host)]
+
+        def flush():
+            # queue the pending results' copies to host (behind their own sets' work)
+            while pending:
+                j, res, ev = pending.pop(0)
+                self.out_stream.wait_event(ev)
+                with torch.cuda.stream(self.out_stream):
+                    outputs[j].copy_(res, non_blocking=True)
+                    e = torch.cuda.Event()
+                    e.record(self.out_stream)
+                res.record_stream(self.out_stream)  # kept until its copy is done
+                copies.append((j, e))
+
         for i in range(n):
             info = new_info()
             nxt: dict = {}
 
             def hook(after, j=i + 1):
+                flush()  # set i-1's result: its copy runs under set i's k-NN
+                if j >= n:
+                    return None
                 # set j's redistribution under set i's k-NN (issued right after the k-NN
                 # launch), once set j's points are on the device
                 redist.wait_stream(after)
                 redist.wait_stream(self.copy_stream)
                 with torch.cuda.stream(redist):
                     nxt["P"] = PL.redistribute_set(self._dbuf[j % 2], comm, cfg, n_totals[j])
+                    e = torch.cuda.Event()
+                    e.record(redist)
+                red_ev[j % 2] = e
                 if self.build_ahead:
                     # and its index, on a stream of its own (the collectives' stream, which
                     # set i's halo exchange and result return wait for, stays short)
@@ -292,26 +382,19 @@ class SetStream:
                 return redist
 
             with trace.range(f"lsknn:set {i}"):
-                res = PL.compute_set(P, comm, cfg, info, hook=hook if i + 1 < n else None)
-            self.out_stream.wait_stream(cur)
+                res = PL.compute_set(P, comm, cfg, info, hook=hook)
             ev = torch.cuda.Event()
-            with torch.cuda.stream(self.out_stream):
-                outputs[i].copy_(res, non_blocking=True)
-                ev.record(self.out_stream)
-            res.record_stream(self.out_stream)  # kept until its copy is done
+            ev.record(cur)
+            pending.append((i, res, ev))
             del res
-            cur.synchronize()
-            redist.synchronize()
-            if i + 2 < n:  # the buffer set i was redistributed from is free again
-                self._prefetch(i + 2, inputs[i + 2])
-            cur.wait_stream(redist)
+            if i + 2 < n:  # the buffer set i was redistributed from, once that is done
+                self._prefetch_after(i + 2, inputs[i + 2], red_ev[i % 2])
+            cur.wait_stream(redist)  # set i+1's points are redistributed (device-side wait)
             P = nxt.get("P")
             self.last_info = info
-            fin.append((i, ev))
-            while len(fin) > 1:  # set i-1's copy was queued before set i's
-                j, e = fin.pop(0)
-                e.synchronize()
-                done(j)
-        torch.cuda.synchronize(dev)  # the last results are in host memory
-        for j, _ in fin:
+            while copies and copies[0][1].query():  # finished sets, without waiting
+                done(copies.pop(0)[0])
+        flush()
+        for j, e in copies:
+            e.synchronize()
             done(j)

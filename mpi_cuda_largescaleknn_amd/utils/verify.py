@@ -77,8 +77,10 @@ def count_below(pts: torch.Tensor, q: torch.Tensor, thr: torch.Tensor, counts: t
             part = pts[s:s + chunk]
             part = part.to(dev, non_blocking=True) if part.device != dev else part
             part = part.contiguous()
-            K.check(lib.lsk_hip_count_below(part.data_ptr(), part.shape[0], q.data_ptr(), thr.data_ptr(), nq,
-                                            counts.data_ptr(), K._stream(part)), "count_below")
+            for j in range(0, nq, 1024):  # (the kernel takes <= 1024 queries per launch)
+                m = min(1024, nq - j)
+                K.check(lib.lsk_hip_count_below(part.data_ptr(), part.shape[0], q[j:].data_ptr(), thr[j:].data_ptr(),
+                                                m, counts[j:].data_ptr(), K._stream(part)), "count_below")
         return
     c = np.zeros((nq, 2), dtype=np.uint64)
     p = pts.contiguous().float()

@@ -1,4 +1,4 @@
-"""MFMA vs VALU screening A/B (csrc/hip/screen_ab.hip) on the production data layout.
+"""MFMA vs VALU screening A/B (scripts/micro/screen_ab.hip) on the production data layout.
 
     python scripts/mfma_screen_ab.py [--points 1e8] [--steps 64] [--k 100]
 

@@ -155,8 +155,7 @@ __global__ __launch_bounds__(kThreads) void screen_mfma_kernel(const float *__re
 extern "C" int lsk_hip_screen_ab(const float *pts, int64_t n, const float *thr, int steps, int mode,
                                  uint32_t *out, uint32_t *viol, void *stream) {
   if (n < 64 || n % 64 != 0 || steps < 1 || mode < 0 || mode > 2) {
-    lsk::set_last_error("screen_ab: n must be a positive multiple of 64, steps >= 1, mode 0..2");
-    return 1;
+    return 1;  // n must be a positive multiple of 64, steps >= 1, mode 0..2
   }
   const unsigned nb = lsk_blocks(n, kThreads);
   hipStream_t st = (hipStream_t)stream;
@@ -166,6 +165,5 @@ extern "C" int lsk_hip_screen_ab(const float *pts, int64_t n, const float *thr, 
     screen_mfma_kernel<false><<<nb, kThreads, 0, st>>>(pts, n, thr, steps, out, viol);
   else
     screen_mfma_kernel<true><<<nb, kThreads, 0, st>>>(pts, n, thr, steps, out, viol);
-  LSK_CHECK_LAUNCH("screen_ab");
-  return 0;
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }

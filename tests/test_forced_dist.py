@@ -30,6 +30,7 @@ def _worker(rank, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=0, world_size=1)
     comm = TorchComm("cpu", force=True)
+    PL.HALO_ONE_RANK = True  # exercise the (empty) halo exchange too
     p = clustered(6000, seed=2)
     cfg = E.KnnConfig(k=12)
     res = {}
@@ -39,6 +40,10 @@ def _worker(rank, port, out_dir):
         res[name] = fn(p, comm, cfg, info)
         res[name + "_single"] = fn(p, SingleComm("cpu"), cfg)
         res[name + "_phases"] = sorted(info.timer.times)
+    PL.HALO_ONE_RANK = False  # default: a 1-rank group skips the halo
+    info = PL.RunInfo(PL.PhaseTimer(True, torch.device("cpu")))
+    res["nohalo"] = PL.prepartitioned_knn(p, comm, cfg, info)
+    res["nohalo_phases"] = sorted(info.timer.times)
     torch.save(res, os.path.join(out_dir, "res.pt"))
     dist.destroy_process_group()
 
@@ -49,7 +54,9 @@ def test_forced_one_rank_gloo_equals_single(tmp_path):
     for name in ("unordered", "prepartitioned", "ring", "peer"):
         assert torch.equal(res[name], res[name + "_single"]), name
     assert "alltoallv_points" in res["unordered_phases"]
-    assert "knn_local+halo_exchange" in res["prepartitioned_phases"]  # overlapped halo (default)
+    assert "knn_local+halo_exchange" in res["prepartitioned_phases"]  # overlapped halo
+    assert torch.equal(res["nohalo"], res["prepartitioned_single"])
+    assert "knn_local" in res["nohalo_phases"] and "knn_local+halo_exchange" not in res["nohalo_phases"]
 
 
 def _chunk_worker(rank, size, port, out_dir):

@@ -43,15 +43,22 @@ def test_graph_replay_matches_eager_on_new_data(variant, k):
     torch.cuda.current_stream(DEV).wait_stream(side)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
+    E.reset_kernels_used()
     with torch.cuda.graph(g):
         body()
     torch.cuda.synchronize()
+    # the captured build decides grid vs rows on the device (knn_engine.build_grid)
+    assert len(E.GATES_SEEN) == 1
+    gate = E.GATES_SEEN[0]
 
-    for data in (uniform(n, seed=1), clustered(n, seed=2), uniform(n, seed=3) * 7.0 - 2.0):
+    for data, grid in ((uniform(n, seed=1), True), (clustered(n, seed=2), None),
+                       (uniform(n, seed=3) * 7.0 - 2.0, True)):
         host_pts.copy_(data)
         host_out.fill_(-1.0)
         g.replay()
         torch.cuda.synchronize()
+        if grid:
+            assert int(gate.item()) == 1  # uniform data: the captured grid kernel ran
         ref = E.knn_distances(data.to(DEV), k).cpu()
         assert torch.equal(host_out, ref)
 

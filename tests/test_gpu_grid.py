@@ -109,11 +109,82 @@ def test_grid_auto_skips_crowded_data():
     E.GRID = "auto"
     try:
         idx = E.build_index(p, grid=True)
-        assert idx.grid is None
+        assert idx.grid is not None and not idx.grid.applies()  # the device said no
+        got = torch.empty(idx.n, dtype=torch.float32, device=DEV)
+        E.reset_kernels_used()
+        E.query(idx, E.KnnConfig(k=16), E.radius_hint(idx.box, idx.n, 16), final_out=got)
+        assert E.kernels_used() == ["rows"]
+        assert torch.equal(got.cpu(), oracle(p.cpu(), 16))
         idx = E.build_index(uniform(200_000, seed=2).to(DEV), grid=True)
-        assert idx.grid is not None
+        assert idx.grid is not None and idx.grid.applies()
     finally:
         E.GRID = old
+
+
+def test_grid_level_from_counts():
+    """The host picks the level from the point counts (no census read): the census's
+    choice for uniform data, capped by the local table size."""
+    assert [E.grid_level_for(n, n) for n in (10_000_000, 100_000_000, 1_000_000_000)] == [7, 8, 9]
+    # a rank's share of a 3.2B-point global cube: level 10 would be a 16 GiB table
+    assert E.grid_level_for(3_200_000_000, 100_000_000) == 9
+    assert E.grid_level_for(1_000_000_000, 125_000_000) == 9
+
+
+def _rows_output(idx, k):
+    grid, idx.grid = idx.grid, None
+    try:
+        out = torch.empty(idx.n, dtype=torch.float32, device=DEV)
+        E.query(idx, E.KnnConfig(k=k), E.radius_hint(idx.box, idx.n, k), final_out=out)
+        return out
+    finally:
+        idx.grid = grid
+
+
+def _sampled(p, out, k, nsamp):
+    from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm
+    from mpi_cuda_largescaleknn_amd.utils import verify as V
+
+    r = V.sampled_exact(SingleComm(torch.device(DEV)), p, out, 0, p.shape[0], k, nsamp=nsamp)
+    assert r["exact"] == r["samples"] >= min(nsamp, p.shape[0]) * 0.99, r
+
+
+@pytest.mark.parametrize("k", [16, 100])
+def test_grid_production_level_1e8(k):
+    """1e8 uniform points: the level the 1e8 bench runs at (grandchildren at level 8). The
+    grid kernel's whole output equals the bucket-tree kernel's bit for bit, and 131072
+    sampled outputs are exact against all 1e8 points (brute-force counts)."""
+    n = 100_000_000
+    g = torch.Generator(device=DEV).manual_seed(123 + k)
+    p = torch.rand((n, 3), generator=g, device=DEV)
+    idx = E.build_index(p, grid=True)
+    assert idx.grid is not None and idx.grid.level + 2 == 8 and idx.grid.applies()
+    out = torch.empty(n, dtype=torch.float32, device=DEV)
+    st = E.KnnStats()
+    E.query(idx, E.KnnConfig(k=k), E.radius_hint(idx.box, n, k), stats=st, final_out=out)
+    assert st.counters.get("failed_lanes", 0) == 0 and st.counters.get("fallback_queries", 0) == 0
+    assert torch.equal(out, _rows_output(idx, k))
+    del idx
+    _sampled(p, out, k, 1 << 17)
+
+
+@pytest.mark.parametrize("k", [16, 100])
+def test_grid_forced_level9_subcube(k):
+    """Grandchildren at level 9 (the 1B bench's level) on 2e7 points in a 1/64 sub-cube of
+    the key cube (eight far corner points span the cube): same density per cell as 1B
+    uniform points. Whole output grid == rows bitwise, plus exact samples."""
+    n = 20_000_000
+    g = torch.Generator(device=DEV).manual_seed(77 + k)
+    p = torch.rand((n, 3), generator=g, device=DEV) * 0.25
+    corners = torch.tensor([[x, y, z] for x in (0.0, 1.0) for y in (0.0, 1.0) for z in (0.0, 1.0)],
+                           device=DEV)
+    p[:8] = corners
+    idx = E.build_index(p, grid=True, grid_level=9)
+    assert idx.grid.level + 2 == 9 and idx.grid.applies()
+    out = torch.empty(n, dtype=torch.float32, device=DEV)
+    E.query(idx, E.KnnConfig(k=k), E.radius_hint(idx.box, n, k), final_out=out)
+    assert torch.equal(out, _rows_output(idx, k))
+    del idx
+    _sampled(p, out, k, 1 << 14)
 
 
 def test_grid_knn_large_k_counter_wraps():

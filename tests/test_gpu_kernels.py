@@ -348,25 +348,30 @@ def test_segment_bounds_kernel_matches_torch():
 
 @pytest.mark.parametrize("dist", ["uniform", "clustered", "mixed_scale"])
 def test_mfma_screen_is_conservative(dist):
-    """screen_ab.hip: the MFMA 16x16x4 screen (row-centred |q'|^2 - 2q'.p' + |p'|^2 with an
+    """scripts/micro/screen_ab.hip (the measured-and-rejected MFMA experiment): the MFMA 16x16x4 screen (row-centred |q'|^2 - 2q'.p' + |p'|^2 with an
     f32 error margin) never drops a (query, candidate) pair whose canonical d^2 is below
     the threshold, keeps few extra pairs, and the VALU form counts exactly
     the canonical pairs. mixed_scale puts the points near 500 (large coordinates, tiny
     distances: the centring is what keeps the margin small)."""
-    from mpi_cuda_largescaleknn_amd import _native
+    import ctypes as C
+
+    from mpi_cuda_largescaleknn_amd import _build
 
     n, steps = 1 << 16, 24
     p = GENERATORS[dist](n).to(DEV)
     idx = E.build_index(p)
     sp = idx.pts[:n].contiguous()
     thr = (E.knn_distances(sp, 16).double() ** 2 * 1.5).float().contiguous()
-    lib = _native.hip()
+    lib = C.CDLL(_build.micro_lib("screen_ab"))  # scripts/micro/screen_ab.hip (an experiment)
+    lib.lsk_hip_screen_ab.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]
     outs = []
     viol = torch.zeros(1, dtype=torch.int32, device=DEV)
     for mode in (0, 1, 2):
         out = torch.zeros(n, dtype=torch.int32, device=DEV)
-        K.check(lib.lsk_hip_screen_ab(sp.data_ptr(), n, thr.data_ptr(), steps, mode, out.data_ptr(),
-                                      viol.data_ptr(), K._stream(sp)), "screen_ab")
+        rc = lib.lsk_hip_screen_ab(sp.data_ptr(), n, thr.data_ptr(), steps, mode, out.data_ptr(),
+                                   viol.data_ptr(), K._stream(sp))
+        assert rc == 0, f"screen_ab: {rc}"
         outs.append(int(out.long().sum()))
     torch.cuda.synchronize()
     assert int(viol.item()) == 0

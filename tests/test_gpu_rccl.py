@@ -41,6 +41,7 @@ def _worker(rank, port, out_dir):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, pg_options=opts)
     comm = TorchComm(dev, force=True)
     assert comm.backend == "nccl" and comm.distributed and not comm.staged
+    PL.HALO_ONE_RANK = True  # the halo all-gather / all-to-all-v on RCCL too (no peer)
     one = SingleComm(dev)
     p = clustered(60000, seed=11).to(dev)
     cfg = E.KnnConfig(k=24)
@@ -116,6 +117,7 @@ def _native_worker(rank, lib, out_dir):
     torch.cuda.set_device(dev)
     path = None if lib == "rocm" else os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
     comm = RcclComm(dev, 0, 1, dist.HashStore(), force=True, lib_path=path)
+    PL.HALO_ONE_RANK = True
     one = SingleComm(dev)
     res = {"version": comm.version, "path": comm.lib_path}
     t = torch.tensor([3.0, -1.0, 7.0], device=dev)

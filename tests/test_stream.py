@@ -46,6 +46,32 @@ def test_stream_loopback_cpu(size):
         assert torch.equal(got, oracle(p, k)), i
 
 
+@pytest.mark.parametrize("size", [1, 2, 3])
+def test_stream_prepartitioned_loopback_cpu(size):
+    """variant="prepartitioned": every rank's set is its own spatial slab (a file per
+    rank); the concatenated outputs equal the oracle of the union, set by set."""
+    k = 9
+    cfg = E.KnnConfig(k=k, publish_levels=4)
+    S = [GENERATORS["uniform"](4000, seed=4), GENERATORS["clustered"](5000, seed=8)]
+    slabs = []
+    for p in S:
+        order = torch.argsort(p[:, 0], stable=True)  # x slabs: one "file" per rank
+        slabs.append(p[order].contiguous())
+
+    def fn(comm):
+        ins, outs = [], []
+        for p in slabs:
+            b, e = p.shape[0] * comm.rank // comm.size, p.shape[0] * (comm.rank + 1) // comm.size
+            ins.append(p[b:e].contiguous())
+            outs.append(torch.empty(e - b, dtype=torch.float32))
+        SetStream(comm, cfg, variant="prepartitioned").run(ins, outs)
+        return outs
+
+    per_rank = run_loopback(size, fn)
+    for i, p in enumerate(slabs):
+        assert torch.equal(torch.cat([per_rank[r][i] for r in range(size)]), oracle(p, k)), i
+
+
 def test_stream_length_mismatch():
     with pytest.raises(ValueError):
         SetStream(SingleComm("cpu"), E.KnnConfig(k=4)).run([torch.zeros(10, 3)], [])
@@ -154,3 +180,62 @@ def test_stream_lazy_sets_and_on_done_cpu():
 @pytest.mark.parametrize("direct", [True, False])
 def test_stream_lazy_sets_and_on_done_gpu(direct):
     _check_lazy_stream(torch.device("cuda", torch.cuda.current_device()), True, direct)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ahead", [False, True])
+def test_stream_failure_overflow_rerun_gpu(ahead, monkeypatch):
+    """every k-NN launch hands every 7th query to the backstop and the failure
+    list holds only 16, so every set's failure word overflows and the host reruns the
+    whole set on the exact kernel while the next set is already queued — set i's output
+    copy must follow that rerun (SetStream._release), in the default and the build-ahead
+    modes, with lazy inputs / outputs released in on_done."""
+    from mpi_cuda_largescaleknn_amd.ops import kernels as KK
+
+    monkeypatch.setattr(E, "DEBUG_FAIL_MOD", 7)
+    monkeypatch.setattr(KK, "FAIL_CAP_OVERRIDE", 16)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    k = 12
+    S = sets() + [GENERATORS["uniform"](40_000, seed=9)]
+    ins = _Lazy(lambda i: S[i].pin_memory(), len(S))
+    outs = _Lazy(lambda i: torch.full((S[i].shape[0],), -1.0).pin_memory(), len(S))
+    done = []
+
+    def on_done(i):
+        assert torch.equal(outs[i], oracle(S[i], k)), i
+        done.append(i)
+        ins.alive.pop(i)
+        outs.alive.pop(i)
+
+    SetStream(SingleComm(dev), E.KnnConfig(k=k), direct_out=False, build_ahead=ahead).run(ins, outs, on_done=on_done)
+    assert done == list(range(len(S)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])
+@pytest.mark.parametrize("size", [2, 3])
+def test_stream_distributed_loopback_gpu(variant, size):
+    """The multi-rank stream on the GPU (loopback ranks as threads sharing cuda:0): next
+    set's redistribution under the current k-NN, result copies under the next set, no
+    host sync between sets; every set equals the oracle and on_done runs in order."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    k = 10
+    cfg = E.KnnConfig(k=k, publish_levels=6)
+    S = [GENERATORS["uniform"](20_000, seed=1), GENERATORS["clustered"](15_000, seed=2),
+         GENERATORS["uniform"](25_000, seed=3)]
+    if variant == "prepartitioned":
+        S = [p[torch.argsort(p[:, 0], stable=True)].contiguous() for p in S]
+
+    def fn(comm):
+        ins, outs, order = [], [], []
+        for p in S:
+            b, e = p.shape[0] * comm.rank // comm.size, p.shape[0] * (comm.rank + 1) // comm.size
+            ins.append(p[b:e].contiguous().pin_memory())
+            outs.append(torch.full((e - b,), -1.0).pin_memory())
+        SetStream(comm, cfg, variant=variant).run(ins, outs, on_done=order.append)
+        assert order == list(range(len(S)))
+        return outs
+
+    per_rank = run_loopback(size, fn, dev)
+    for i, p in enumerate(S):
+        assert torch.equal(torch.cat([per_rank[r][i] for r in range(size)]), oracle(p, k)), i
