@@ -181,6 +181,17 @@ def main():
         raise RuntimeError("bench.py: no GPU available (use --device cpu for a rehearsal)")
     n_total = int(args.points)
     cfg = KnnConfig(k=args.k, collect_stats=args.stats)
+    if args.mode != "halo":
+        # the reference's heaps (N/P*k*8 B per rank) must fit before any point is made
+        b0, e0 = block_range(n_total, rank, world)
+        cap = (torch.cuda.get_device_properties(device).total_memory if device.type == "cuda"
+               else int(float(os.environ.get("LSKNN_REF_CAPACITY_GB", "288")) * 1e9))
+        try:
+            RA.check_ref_fits(e0 - b0, args.k, cap, world)
+        except ValueError as e:
+            sys.stderr.write(f"bench.py: {e}\n")
+            LA.finalize(launch)
+            sys.exit(3)
 
     # pipelined stream of point sets (see --pipeline): two different synthetic sets alternate
     # (auto: from 1e7 points; below that one HIP-graph replay per set is cheaper than the

@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 6  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 7  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -88,6 +88,7 @@ class KnnArgs(C.Structure):
         ("gate", vp),
         ("gate_on", C.c_int32),
         ("pad2", C.c_int32),
+        ("ngroups_dev", vp),
     ]
 
 
@@ -169,6 +170,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_knn_grid": ([C.POINTER(KnnArgs), C.POINTER(GridView), vp], i32),
         "lsk_hip_grid_decide": ([vp, vp, i64, i32, C.c_float, i32, vp, vp], i32),
+        "lsk_hip_boundary_groups": ([vp, i32, i64, vp, vp, vp, C.c_int, C.c_int, vp, vp], i32),
         "lsk_hip_grid_build": ([vp, vp, i64, vp, i32, vp, vp], i32),
         "lsk_hip_key_levels": ([vp, i64, vp, vp], i32),
         "lsk_hip_grid_sq": ([vp, i64, vp, vp], i32),

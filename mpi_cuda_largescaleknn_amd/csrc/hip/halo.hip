@@ -156,6 +156,64 @@ __global__ __launch_bounds__(256) void flag_groups_inverse_kernel(const float *_
   }
 }
 
+// gap² between two node boxes (8 floats each: lo.xyz, -, hi.xyz, -). For q in box a and
+// p in box b every axis gap is at most |q - p| on that axis after rounding (float
+// subtraction is monotone), so with the canonical dist2 the result is <= dist2(q, p).
+__device__ __forceinline__ float box_box_gap2(const float *a, const float *b) {
+  const float gx = fmaxf(0.f, fmaxf(a[0] - b[4], b[0] - a[4]));
+  const float gy = fmaxf(0.f, fmaxf(a[1] - b[5], b[1] - a[5]));
+  const float gz = fmaxf(0.f, fmaxf(a[2] - b[6], b[2] - a[6]));
+  return lsk::dist2(gx, gy, gz);
+}
+
+// One lane per local bucket (query group): its leaf box and squared radius bound (lo.w)
+// against every other rank's published tree, wave-uniform DFS as halo_mask_kernel.
+__global__ __launch_bounds__(256) void boundary_groups_kernel(const float *__restrict__ lnodes, int32_t depth,
+                                                              int64_t ngroups, const float *__restrict__ pub,
+                                                              const int64_t *__restrict__ pub_off,
+                                                              const int32_t *__restrict__ pub_depth, int nranks,
+                                                              int self, uint32_t *__restrict__ flags) {
+  __shared__ uint32_t stack[4][kStack];
+  const int wid = threadIdx.x >> 6, lane = lsk::lane_id();
+  const int64_t g = ((int64_t)lsk::xcd_remap(blockIdx.x, gridDim.x) * 4 + wid) * 64 + lane;
+  if (__ballot(g < ngroups) == 0) return;
+  const bool valid = g < ngroups;
+  float box[8];
+  const float *lf = lnodes + 8 * (size_t)(((int64_t)1 << depth) + (valid ? g : 0));
+#pragma unroll
+  for (int t = 0; t < 8; t++) box[t] = lf[t];
+  const float r2 = valid ? box[3] : 0.f;
+  bool hit = false;
+  for (int j = 0; j < nranks; j++) {
+    if (j == self) continue;
+    const float *nodes = pub + pub_off[j];
+    const uint32_t leaf0 = 1u << (uint32_t)pub_depth[j];
+    uint32_t sp = 0;
+    if (lane == 0) stack[wid][0] = 1u;
+    sp = 1;
+    while (sp > 0) {
+      sp--;
+      const uint32_t node = lsk::uniform(stack[wid][sp]);
+      const float *nd = nodes + 8 * (size_t)node;
+      const bool need = valid && !hit && box_box_gap2(box, nd) < r2;
+      if (!__ballot(need)) continue;
+      if (node >= leaf0) {
+        hit = hit || need;
+        if (__ballot(valid && !hit) == 0) break;
+        continue;
+      }
+      if (sp + 2 > kStack) break;  // cannot happen for depth < 32
+      if (lane == 0) {
+        stack[wid][sp] = 2 * node + 1;
+        stack[wid][sp + 1] = 2 * node;
+      }
+      sp += 2;
+    }
+    if (__ballot(valid && !hit) == 0) break;
+  }
+  if (valid) flags[g] = hit ? 1u : 0u;
+}
+
 __global__ __launch_bounds__(256) void compact_kernel(const uint32_t *__restrict__ flags,
                                                       int64_t n, uint32_t *__restrict__ list,
                                                       uint32_t *__restrict__ count) {
@@ -227,6 +285,20 @@ extern "C" int lsk_hip_halo_mask(const float *pts, int64_t n, const float *pub,
                                                                       pub_depth, nranks, self,
                                                                       mask);
   LSK_CHECK_LAUNCH("halo_mask");
+  return 0;
+}
+
+extern "C" int lsk_hip_boundary_groups(const float *local_nodes, int32_t depth, int64_t ngroups, const float *pub,
+                                       const int64_t *pub_off, const int32_t *pub_depth, int nranks, int self,
+                                       uint32_t *flags, void *stream) {
+  if (ngroups <= 0) return 0;
+  if (nranks > 64 || depth < 0 || depth > 30) {
+    lsk::set_last_error("boundary_groups: at most 64 ranks, tree depth in [0, 30]");
+    return 1;
+  }
+  boundary_groups_kernel<<<lsk_blocks(ngroups, 256), 256, 0, (hipStream_t)stream>>>(
+      local_nodes, depth, ngroups, pub, pub_off, pub_depth, nranks, self, flags);
+  LSK_CHECK_LAUNCH("boundary_groups");
   return 0;
 }
 

@@ -208,7 +208,9 @@ __global__ __launch_bounds__(kWaves * 64) void knn_exact_kernel(const lsk_knn_ar
     const int64_t c = (int64_t)count[0];
     total = c < cap ? c : cap;
   } else {
-    total = A.groups ? A.ngroups * lsk::kBucket : A.nq;
+    int64_t ng = A.ngroups;
+    if (A.groups && A.ngroups_dev) ng = min(ng, (int64_t)A.ngroups_dev[0]);
+    total = A.groups ? ng * lsk::kBucket : A.nq;
   }
   for (int64_t i = gw; i < total; i += tw) {
     int64_t qi;

@@ -727,10 +727,13 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   const int lane = lsk::lane_id();
   const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
   const uint64_t wave = (uint64_t)blk * kWPB + wid;
-  const uint64_t ngroups = (uint64_t)((A.nq + 63) / 64);
+  const uint64_t ngroups = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
   if (wave >= ngroups) return;
+  if (A.groups && A.ngroups_dev && wave >= (uint64_t)*A.ngroups_dev) return;
   if (A.gate && *A.gate != A.gate_on) return;  // the device chose knn_rows
-  const int64_t q0 = (int64_t)wave * lsk::kBucket;
+  // a listed group (the boundary / interior passes of a distributed run) or the wave's own
+  const uint32_t grp = lsk::uniform(A.groups ? A.groups[wave] : (uint32_t)wave);
+  const int64_t q0 = (int64_t)grp * lsk::kBucket;
   const int64_t qi = q0 + lane;
   const bool valid = qi < A.nq;
   const uint32_t nvalid = (uint32_t)((A.nq - q0) < lsk::kBucket ? (A.nq - q0) : lsk::kBucket);
@@ -1170,13 +1173,13 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
     lsk::set_last_error("knn_grid: k must be in [1, 65535]");
     return 1;
   }
-  if (A.nq >= ((int64_t)1 << 32) || A.ntrees != 1 || A.groups || A.init_d2 ||
-      A.tree[0].n >= ((int64_t)1 << 32) || !grid || grid->level < 0 || grid->level > 8) {
-    lsk::set_last_error("knn_grid: one tree (< 2^32 points, the queries' own), no groups / init_d2, "
+  if (A.nq >= ((int64_t)1 << 32) || A.ntrees != 1 || A.init_d2 || A.tree[0].n >= ((int64_t)1 << 32) ||
+      !grid || grid->level < 0 || grid->level > 8) {
+    lsk::set_last_error("knn_grid: one tree (< 2^32 points, the queries' own), no init_d2, "
                         "grid level in [0, 8]");
     return 1;
   }
-  const int64_t ngroups = (A.nq + 63) / 64;
+  const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
   knn_grid_kernel<<<lsk_blocks(ngroups, kWPB), kThreads, 0, (hipStream_t)stream>>>(A, *grid);
   LSK_CHECK_LAUNCH("knn_grid");

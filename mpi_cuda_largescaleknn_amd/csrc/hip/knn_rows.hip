@@ -1039,6 +1039,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid;
   const uint64_t ngroups = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
   if (wave >= ngroups) return;
+  if (A.groups && A.ngroups_dev && wave >= (uint64_t)*A.ngroups_dev) return;
   if (A.gate && *A.gate != A.gate_on) return;  // the device chose the grid kernel
   const uint32_t g = lsk::uniform(A.groups ? A.groups[wave] : (uint32_t)wave);
   const int64_t q0 = (int64_t)g * lsk::kBucket;

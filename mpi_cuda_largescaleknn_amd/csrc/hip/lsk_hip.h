@@ -128,6 +128,8 @@ typedef struct lsk_knn_args {
   const int32_t *gate;      // optional device flag (lsk_hip_grid_decide): the rows / grid
   int32_t gate_on;          // kernel runs only when *gate == gate_on (else every wave
   int32_t pad2;             // returns at once): both are queued, the device picks one
+  const uint32_t *ngroups_dev;  // optional, with `groups`: the list's length on the device
+                                // (ngroups is then the launch's upper bound; no host read)
 } lsk_knn_args;
 
 // Production kernel: 4 x 16-query rows, 16-bit LDS histogram radix select. Queries it
@@ -177,6 +179,14 @@ int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *
 // Published tree: the top `levels` levels of a tree (node slots 1 .. 2^levels-1... up to
 // 2^(levels+1)), each node 8 floats (lo.xyz, r2, hi.xyz, pad).
 // mask[i] bit j set iff point i must be sent to rank j (j != self).
+// Boundary classification of the local query groups before the local pass: flags[g] = 1
+// iff the box of local bucket g (leaf of local_nodes, depth `depth`), inflated by its
+// squared radius bound lo.w, comes strictly closer than that bound to some node of
+// another rank's published tree — i.e. some other rank's point could be among the k
+// nearest of one of the group's queries. flags[g] = 0 groups need no halo at all.
+int lsk_hip_boundary_groups(const float *local_nodes, int32_t depth, int64_t ngroups, const float *pub,
+                            const int64_t *pub_off, const int32_t *pub_depth, int nranks, int self,
+                            uint32_t *flags, void *stream);
 int lsk_hip_halo_mask(const float *pts, int64_t n, const float *pub, const int64_t *pub_off,
                       const int32_t *pub_depth, int nranks, int self, uint64_t *mask,
                       void *stream);

@@ -399,7 +399,8 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
           groups: torch.Tensor | None = None, ngroups: int = 0, out: torch.Tensor | None = None,
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
           init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None,
-          keep_d2: bool = False, deferred: list | None = None) -> torch.Tensor:
+          keep_d2: bool = False, deferred: list | None = None,
+          ngroups_dev: torch.Tensor | None = None) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
     `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order.
 
@@ -409,7 +410,9 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
 
     `deferred` (a list): the failure-word read (a host sync) is not done here but queued
     on the list; `settle(deferred)` does it later — the launch stays asynchronous, so the
-    host can queue other work (the overlapped halo exchange) behind it."""
+    host can queue other work (the overlapped halo exchange) behind it.
+    `ngroups_dev` (with `groups`): the list's length as an int32 [1] tensor (on the GPU it
+    stays on the device; `ngroups` is then the launch's upper bound)."""
     n = index.n
     want_d2 = final_out is None or keep_d2 or out is not None
     if out is None and want_d2:
@@ -427,6 +430,8 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
             rows = None
             KERNELS_USED.add("cpu")
         else:
+            if ngroups_dev is not None:
+                ngroups = int(ngroups_dev.view(-1)[0])
             g = groups[:ngroups].to(torch.int64)
             rows = (g[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
             rows = rows[rows < n]
@@ -442,9 +447,9 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     kw = dict(groups=groups, ngroups=ngroups, seed=SEED_BUCKETS, init_d2=init_d2,
               out_perm=index.perm if final_out is not None else None, out_final=final_out)
     impl = KNN_IMPL
-    use_grid = (impl == "rows" and index.grid is not None and len(trees) == 1 and groups is None
+    use_grid = (impl == "rows" and index.grid is not None and len(trees) == 1
                 and init_d2 is None and cfg.k <= K.ROWS_MAX_K)
-    if groups is None:  # (a whole-set pass, not a halo re-query)
+    if len(trees) == 1 and init_d2 is None:  # (a local pass, not a halo re-query)
         if use_grid and index.grid.gate is not None:
             GATES_SEEN.append(index.grid.gate)  # grid or rows: resolved by kernels_used()
             del GATES_SEEN[:-1024]  # (reporting only: a long stream keeps the last sets)
@@ -452,14 +457,15 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
             KERNELS_USED.add("grid" if use_grid else impl)
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
-                   grid=index.grid.view() if use_grid else None, **kw)
+                   grid=index.grid.view() if use_grid else None, ngroups_dev=ngroups_dev, **kw)
     def check() -> bool:
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun
         # the whole query on the exact kernel (on the current stream; returns True then)
         nfail = fw.value()
         rerun = nfail > fw.cap
         if rerun:
-            K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", **kw)
+            K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", ngroups_dev=ngroups_dev,
+                      **kw)
         if stats is not None:
             stats.add_fallback(nfail)
             stats.add(raw)

@@ -292,7 +292,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
-            debug_fail_mod: int = 0, grid=None) -> FailWord:
+            debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -306,6 +306,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     out_perm / out_final (optional, fused scatter): the kernels also write
     out_final[out_perm[q]] = final distance; out_d2 may then be None.
     debug_fail_mod (tests): the rows kernel also fails every query q with q % mod == 0.
+    ngroups_dev (optional, with groups): int32 [1] on the device, the list's length
+    (ngroups is then only the launch's upper bound).
     grid (impl "grid"): (slots, level, box, inf4[, gate]) of knn_engine.GridIndex — the
     cell-grid candidate source of knn_grid.hip for one tree whose points are the queries
     (same failure list and backstop as "rows"); with a device gate (int32 [1]) the grid
@@ -319,13 +321,14 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
         raise ValueError("knn_gpu: out_perm must be int32 [>= nq], out_final float32")
     if impl not in ("rows", "exact", "grid"):
         raise ValueError(f"knn_gpu: impl must be rows, exact or grid, not {impl!r}")
-    if impl == "grid" and (grid is None or len(trees) != 1 or groups is not None or init_d2 is not None):
-        raise ValueError("knn_gpu: impl grid needs a grid, one tree, no groups and no init_d2")
+    if impl == "grid" and (grid is None or len(trees) != 1 or init_d2 is not None):
+        raise ValueError("knn_gpu: impl grid needs a grid, one tree and no init_d2")
     a = KnnArgs()
     a.qpts = _ptr(qpts)
     a.nq = nq
     a.groups = _ptr(groups)
     a.ngroups = ngroups
+    a.ngroups_dev = _ptr(ngroups_dev) if groups is not None else None
     for i, (pts, nodes, qnodes, n, depth) in enumerate(trees):
         a.tree[i] = TreeView(_ptr(pts), _ptr(nodes), _ptr(qnodes), n, depth, 0)
     a.ntrees = len(trees)
@@ -493,6 +496,64 @@ def tree_set_radii_ub(nodes: torch.Tensor, pts: torch.Tensor, n: int, k: int) ->
         ch = nodes[2 * a: 4 * a].view(a, 2, 8)
         nodes[a:2 * a, 3] = torch.maximum(ch[:, 0, 3], ch[:, 1, 3])
     return nodes
+
+
+def boundary_groups(local_nodes: torch.Tensor, depth: int, ngroups: int, pub: torch.Tensor, pub_off: list[int],
+                    pub_depth, self_rank: int) -> torch.Tensor:
+    """int32 [ngroups]: 1 for the local query groups (buckets) whose leaf box, inflated by
+    its squared radius bound (lo.w of local_nodes), comes closer than that bound to some
+    node of another rank's published tree (halo.hip boundary_groups_kernel); 0 = the
+    group's k nearest are all local, whatever the other ranks hold."""
+    nranks = len(pub_off)
+    flags = torch.zeros(max(ngroups, 0), dtype=torch.int32, device=local_nodes.device)
+    if ngroups <= 0:
+        return flags
+    if is_gpu(local_nodes):
+        off = torch.tensor(pub_off, dtype=torch.int64, device=local_nodes.device)
+        dep = (pub_depth.to(device=local_nodes.device, dtype=torch.int32).contiguous()
+               if isinstance(pub_depth, torch.Tensor)
+               else torch.tensor(pub_depth, dtype=torch.int32, device=local_nodes.device))
+        check(_native.hip().lsk_hip_boundary_groups(_ptr(local_nodes), int(depth), int(ngroups), _ptr(pub),
+                                                    _ptr(off), _ptr(dep), nranks, self_rank, _ptr(flags),
+                                                    _stream(local_nodes)), "boundary_groups")
+        return flags
+    # CPU: every group against the leaf level of each published tree, in float64 with the
+    # squared gap shrunk by 2^-20 (a rounding of the canonical float d² cannot hide a
+    # neighbour: the test only errs towards "boundary")
+    if isinstance(pub_depth, torch.Tensor):
+        pub_depth = [int(x) for x in pub_depth.cpu().tolist()]
+    pub = pub.reshape(-1, 8)
+    leaves = local_nodes[(1 << depth):(1 << depth) + ngroups].double()
+    lo, hi, r2 = leaves[:, None, 0:3], leaves[:, None, 4:7], leaves[:, 3]
+    hit = torch.zeros(ngroups, dtype=torch.bool)
+    for j in range(nranks):
+        if j == self_rank:
+            continue
+        d = pub_depth[j]
+        base = pub_off[j] // 8
+        nb = pub[base + (1 << d): base + (2 << d)].double()
+        for s0 in range(0, ngroups, 4096):
+            gap = torch.clamp(torch.maximum(lo[s0:s0 + 4096] - nb[None, :, 4:7], nb[None, :, 0:3] - hi[s0:s0 + 4096]),
+                              min=0.0)
+            g2 = (gap * gap).sum(-1) * (1.0 - 2.0 ** -20)
+            hit[s0:s0 + 4096] |= (g2 < r2[s0:s0 + 4096, None]).any(1)
+    flags[hit] = 1
+    return flags
+
+
+def compact_flags(flags: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(list of the indices i with flags[i] != 0, their count as an int32 [1] tensor on the
+    flags' device: no host read on the GPU)."""
+    n = flags.shape[0]
+    if is_gpu(flags):
+        lst = torch.empty(max(n, 1), dtype=torch.int32, device=flags.device)
+        cnt = torch.zeros(1, dtype=torch.int32, device=flags.device)
+        if n:
+            check(_native.hip().lsk_hip_compact_flags(_ptr(flags), n, _ptr(lst), _ptr(cnt), _stream(flags)),
+                  "compact_flags")
+        return lst, cnt
+    idx = torch.nonzero(flags != 0).view(-1).to(torch.int32)
+    return idx, torch.tensor([idx.shape[0]], dtype=torch.int32)
 
 
 def halo_mask(pts: torch.Tensor, pub: torch.Tensor, pub_off: list[int], pub_depth, self_rank: int) -> torch.Tensor:

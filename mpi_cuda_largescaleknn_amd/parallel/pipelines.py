@@ -377,18 +377,14 @@ def _offsets(counts):
     return o
 
 
-def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo,
-               marks: bool = True) -> torch.Tensor:
-    """Publish the top levels of `radii_nodes` (index's tree with per-node k-th squared
-    radius bounds in lo.w), filter and pack own points for every other rank, exchange:
-    returns the received halo points."""
-    size, rank = comm.size, comm.rank
-    n = index.n
-    dev = index.device
+def _publish(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: E.KnnConfig):
+    """All-gather the top cfg.publish_levels levels of every rank's tree (`radii_nodes`:
+    index's tree with per-node k-th squared radius bounds in lo.w). Returns (pub_all
+    [P, rows, 8], published depths (device int32 [P]), per-rank float offsets)."""
     levels = cfg.publish_levels
     my_levels = min(levels, index.depth)
     rows = 2 << levels
-    pub = torch.zeros((rows, 8), dtype=torch.float32, device=dev)
+    pub = torch.zeros((rows, 8), dtype=torch.float32, device=index.device)
     pub[:, 0:3] = math.inf
     pub[:, 4:7] = -math.inf
     take = min(rows, radii_nodes.shape[0], 2 << my_levels)
@@ -397,10 +393,21 @@ def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: 
     pub[0, 7] = float(my_levels)
     pub_all = comm.allgather(pub)                       # [P, rows, 8]
     depths = pub_all[:, 0, 7].to(torch.int32)           # (device)
+    return pub_all, depths, [j * rows * 8 for j in range(comm.size)]
+
+
+def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo,
+               marks: bool = True) -> torch.Tensor:
+    """Publish the top levels of `radii_nodes` (index's tree with per-node k-th squared
+    radius bounds in lo.w), filter and pack own points for every other rank, exchange:
+    returns the received halo points."""
+    size, rank = comm.size, comm.rank
+    n = index.n
+    dev = index.device
+    pub_all, depths, offs = _publish(index, radii_nodes, comm, cfg)
     if marks:
         info.timer.mark("halo_publish")
     pts = index.pts[:n]
-    offs = [j * rows * 8 for j in range(size)]
     mask = K.halo_mask(pts, pub_all.reshape(-1), offs, depths, rank)
     recv_counts = None
     if K.is_gpu(pts):
@@ -547,37 +554,69 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
         info.timer.mark("knn_local")
         return halo_refine(index, d2, comm, cfg, hint2, info, final_out=final_out)
-    if not gpu:  # same data flow, no streams to overlap on
-        recv = _halo_send(index, _radius_bounds(index, cfg), comm, cfg, info, marks=False)
-        d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True)
-        info.timer.mark("knn_local+halo_exchange")
-        K.tree_set_radii(index.nodes, index.n, d2)
-        return _halo_requery(index, d2, recv, cfg, hint2, info, final_out)
-    dev = index.device
-    cur = torch.cuda.current_stream(dev)
-    comp, side = _overlap_streams(dev)
-    comp.wait_stream(cur)
-    side.wait_stream(cur)
+    n = index.n
+    ng = (n + 63) // 64
+    # 1. boundary groups: a-priori radius bounds (tree_set_radii_ub) against the other
+    #    ranks' published tree tops; a group whose bound keeps it inside this rank's
+    #    region needs no halo at all
+    if gpu:
+        dev = index.device
+        cur = torch.cuda.current_stream(dev)
+        comp, side = _overlap_streams(dev)
+        comp.wait_stream(cur)
+        side.wait_stream(cur)
+        ctx = torch.cuda.stream(comp)
+    else:
+        import contextlib
+        ctx = contextlib.nullcontext()
+    with ctx:
+        ub = _radius_bounds(index, cfg)
+        pub_all, depths, offs = _publish(index, ub, comm, cfg)
+        bflags = K.boundary_groups(ub, index.depth, ng, pub_all, offs, depths, comm.rank)
+        blist, bcnt = K.compact_flags(bflags)
+        ilist, icnt = K.compact_flags(1 - bflags)
+        del ub, bflags
+    if gpu:
+        ev_pub = torch.cuda.Event()
+        ev_pub.record(comp)
+        cur.wait_event(ev_pub)  # (the hook's collectives follow the publish)
     pend: list = []
-    with torch.cuda.stream(comp):
-        d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True, deferred=pend)
-    if hook is not None:
-        # independent work under the k-NN, issued before the halo exchange (whose host
-        # syncs wait for kernels that share the CUs with the k-NN); the halo collectives
-        # follow its collectives (one communicator: never two in flight)
-        st = hook(cur)
-        if st is not None:
-            side.wait_stream(st)
-        hook = None
-    with torch.cuda.stream(side):
-        recv = _halo_send(index, _radius_bounds(index, cfg), comm, cfg, info, marks=False)
-    cur.wait_stream(comp)
-    cur.wait_stream(side)
-    recv.record_stream(cur)
-    d2.record_stream(cur)
-    final_out.record_stream(comp)
-    E.settle(pend)
-    info.counts["halo_overlap"] = 1
+    d2 = torch.zeros(n, dtype=torch.float32, device=index.device)  # interior groups: radius 0 below
+    with ctx:
+        # 2. the boundary groups' local pass first: their exact radii (interior leaves 0)
+        #    are what the other ranks filter their points with
+        E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=blist, ngroups=ng,
+                ngroups_dev=bcnt, deferred=pend if gpu else None)
+        radii = K.tree_set_radii(index.nodes.clone(), n, d2)
+        if gpu:
+            ev_rad = torch.cuda.Event()
+            ev_rad.record(comp)
+        # 3. the interior groups (most of the work) ...
+        if not gpu:
+            recv = _halo_send(index, radii, comm, cfg, info, marks=False)
+        E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=ilist, ngroups=ng,
+                ngroups_dev=icnt, deferred=pend if gpu else None)
+    if gpu:
+        if hook is not None:
+            # independent work under the k-NN (SetStream: the next set's redistribution);
+            # the halo collectives follow its collectives (one communicator: never two in
+            # flight)
+            st = hook(cur)
+            if st is not None:
+                side.wait_stream(st)
+        # ... while the halo is filtered and exchanged on the side stream
+        side.wait_event(ev_rad)
+        with torch.cuda.stream(side):
+            recv = _halo_send(index, radii, comm, cfg, info, marks=False)
+        cur.wait_stream(comp)
+        cur.wait_stream(side)
+        recv.record_stream(cur)
+        d2.record_stream(cur)
+        final_out.record_stream(comp)
+        radii.record_stream(side)
+        E.settle(pend)
+        info.counts["halo_overlap"] = 1
+    info.counts["boundary_groups"] = int(bcnt.view(-1)[0])
     info.timer.mark("knn_local+halo_exchange")
     K.tree_set_radii(index.nodes, index.n, d2)
     return _halo_requery(index, d2, recv, cfg, hint2, info, final_out)

@@ -29,6 +29,32 @@ from .comm import Comm
 from .pipelines import PhaseTimer, RunInfo
 
 
+# Per query and rank, besides its k-heap: the point in the left-balanced tree copy and in
+# the query array (2 x 12 B), its output (4 B) and the builder's tag and sort scratch.
+REF_BYTES_PER_POINT = 40
+REF_SLACK = 2 << 30
+
+
+def ref_memory_bytes(n_local: int, k: int) -> int:
+    """Device bytes a ref-algo rank needs for n_local points: the reference's N·k·8 B of
+    candidate heaps (unorderedDataVariant.cu:168, D4) plus the trees and queries."""
+    return n_local * k * 8 + n_local * REF_BYTES_PER_POINT + REF_SLACK
+
+
+def check_ref_fits(n_local: int, k: int, capacity: int, ranks: int = 1) -> None:
+    """Refuse a ref-algo run whose heaps do not fit (raises ValueError with the arithmetic):
+    the reference allocates N/P·k·8 B of heaps per rank up front and would fail there."""
+    need = ref_memory_bytes(n_local, k)
+    if need > capacity:
+        heaps = n_local * k * 8
+        raise ValueError(
+            f"ref-algo (ring/peer) does not fit: {n_local:,} queries per rank x k={k} x 8 B = "
+            f"{heaps / 1e9:.1f} GB of k-heaps (the reference's N/P*k*8 B, unorderedDataVariant.cu:168) "
+            f"+ {(need - heaps) / 1e9:.1f} GB of trees/queries/scratch = {need / 1e9:.1f} GB > "
+            f"{capacity / 1e9:.1f} GB of device memory per rank; use at least "
+            f"{max(ranks + 1, math.ceil(ranks * need / max(capacity, 1)))} ranks or --mode halo")
+
+
 def ring_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
              overlap: bool = True) -> torch.Tensor:
     """Ring rotation (unorderedDataVariant.cu:173-205), double-buffered: the tree sizes

@@ -220,3 +220,24 @@ def test_bench_self_launch_two_ranks_one_gpu_gloo():
     rec = _json_line(out.stdout)
     assert rec["n_gpus"] == 2 and rec["config"]["ranks"] == 2
     assert rec["config"]["sampled_exact"] == "256/256"
+
+
+def test_bench_ring_refuses_when_heaps_do_not_fit():
+    """--mode ring at 1B on one rank needs 800 GB of the reference's k-heaps (N*k*8 B,
+    unorderedDataVariant.cu:168): refused up front with the arithmetic, before any point
+    is generated; 1e5 points fit."""
+    out = subprocess.run([sys.executable, "bench.py", "--device", "cpu", "--mode", "ring", "--points", "1e9",
+                          "--k", "100", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=_env(),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 3, out.stderr[-2000:]
+    assert "800.0 GB of k-heaps" in out.stderr and "does not fit" in out.stderr
+    assert "{\"metric\"" not in out.stdout
+
+
+def test_ref_memory_arithmetic():
+    from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA
+
+    # the 1B / 8-rank shape fits one MI355X (100 GB of heaps per rank), 1B on one does not
+    RA.check_ref_fits(125_000_000, 100, 288 * 10**9, 8)
+    with pytest.raises(ValueError, match="at least 3 ranks"):
+        RA.check_ref_fits(1_000_000_000, 100, 288 * 10**9, 1)

@@ -153,9 +153,10 @@ def test_unordered_streamed_from_pinned_host(size, monkeypatch):
 
 @pytest.mark.parametrize("k", [16, 100])
 def test_overlapped_halo_gpu_equals_sequential(k, monkeypatch):
-    """The side-stream halo exchange (a-priori radius bounds, publish/filter/pack/exchange
-    while the local k-NN kernel runs) gives the sequential form's bits; its halo is a
-    superset of the sequential one; the overlapped path really ran."""
+    """The side-stream halo exchange (boundary groups from a-priori radius bounds queried
+    first, their exact radii published, filter/pack/exchange while the interior groups'
+    k-NN runs) gives the sequential form's bits; its halo is a subset of the sequential
+    one; the overlapped path really ran."""
     p = clustered(300_000, seed=k)
     ref = single(p, k)
     cfg = E.KnnConfig(k=k)
@@ -173,7 +174,7 @@ def test_overlapped_halo_gpu_equals_sequential(k, monkeypatch):
         res[mode] = (torch.cat([x[0] for x in r]), sum(x[1].counts["halo_recv"] for x in r),
                      [x[1].counts.get("halo_overlap", 0) for x in r])
     assert torch.equal(res[True][0], ref) and torch.equal(res[False][0], ref)
-    assert res[True][1] >= res[False][1]
+    assert res[False][1] >= res[True][1] > 0
     assert res[True][2] == [1, 1, 1, 1] and res[False][2] == [0, 0, 0, 0]
 
 
