@@ -744,7 +744,7 @@ def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int
     hint2 = E.radius_hint(box, n_total, cfg.k)
     info.timer.mark("bounds")
     info.counts["owned_points"] = n_local
-    index = E.build_index(points, box, keys=keys, grid=True)
+    index = E.build_index(points, box, keys=keys, grid=True, density_n=n_total)
     info.timer.mark("build")
     return index, hint2
 
@@ -818,7 +818,7 @@ def unordered_knn(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, info: RunI
     R = redistribute_stream(points, comm, info)
     box, owned = R.box, R.owned
     hint2 = E.radius_hint(box, n_total, cfg.k)
-    index = E.build_index(owned, box, grid=True)
+    index = E.build_index(owned, box, grid=True, density_n=n_total)
     info.timer.mark("build")
     # final distances in received-row order straight from the kernels (fused scatter);
     # the sorted d2 feeds the halo radii and the re-query bounds
@@ -852,6 +852,7 @@ class Redistributed:
     send_counts: list
     index: E.LocalIndex | None = None  # built ahead (SetStream), else by compute_set
     index_ready: object = None         # event after which `index` is complete
+    n_total: int | None = None         # points of the whole set (grid level of the global box)
 
 
 def redistribute_set(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
@@ -867,14 +868,15 @@ def redistribute_set(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total
     hint2 = E.radius_hint(box, n_total, cfg.k)
     info.timer.mark("bounds")
     owned, recv_counts, send_perm, send_counts = redistribute(points, comm, box, info)
-    return Redistributed(int(points.shape[0]), box, hint2, owned, recv_counts, send_perm, send_counts)
+    return Redistributed(int(points.shape[0]), box, hint2, owned, recv_counts, send_perm, send_counts,
+                         n_total=n_total)
 
 
 def build_ahead(P: Redistributed, stream, users) -> None:
     """Build P's index on `stream` (after the work queued there so far) and mark it ready
     with an event; its tensors are kept for the streams in `users` (record_stream)."""
     with torch.cuda.stream(stream):
-        index = E.build_index(P.owned, P.box, grid=True)
+        index = E.build_index(P.owned, P.box, grid=True, density_n=P.n_total)
     P.owned.record_stream(stream)
     for t in (index.pts, index.perm, index.nodes, index.qnodes, index.box) + \
             ((index.grid.slots,) if index.grid is not None else ()):
@@ -899,7 +901,7 @@ def compute_set(P: Redistributed, comm: Comm, cfg: E.KnnConfig, info: RunInfo | 
         if P.index_ready is not None:
             torch.cuda.current_stream(dev).wait_event(P.index_ready)
     else:
-        index = E.build_index(P.owned, P.box, grid=True)
+        index = E.build_index(P.owned, P.box, grid=True, density_n=P.n_total)
     info.timer.mark("build")
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     used: list = []
