@@ -1050,19 +1050,26 @@ __global__ __launch_bounds__(256) void grid_build_kernel(const float *__restrict
 
 // counts[l] += number of i in [1, n) whose key prefix at level l (top 3l bits of the
 // 30-bit key) differs from key i-1's: distinct cells of level l = counts[l] + 1.
+// run > 0: also heavy[0] = 1 if some key equals the key `run` positions before it (an
+// over-full cell, knn_engine.refine_heavy_cells) — the same pass over the keys.
 // Grid-stride: per-thread counts in registers, wave sums, one atomic per level and block.
 constexpr int kLevelsBlocks = 1024;
 __global__ __launch_bounds__(256) void key_levels_kernel(const uint32_t *__restrict__ keys, int64_t n,
-                                                         unsigned long long *__restrict__ counts) {
+                                                         unsigned long long *__restrict__ counts, int64_t run,
+                                                         int32_t *__restrict__ heavy) {
   uint32_t c[11];
 #pragma unroll
   for (int l = 0; l <= 10; l++) c[l] = 0;
+  bool hv = false;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += stride) {
-    const uint32_t x = keys[i - 1] ^ keys[i];  // differing bits
+    const uint32_t ki = keys[i];
+    const uint32_t x = keys[i - 1] ^ ki;  // differing bits
 #pragma unroll
     for (int l = 1; l <= 10; l++) c[l] += (x >> (3 * (10 - l))) != 0u ? 1u : 0u;
+    if (run > 0 && i >= run) hv = hv || keys[i - run] == ki;
   }
+  if (run > 0 && __ballot(hv) && lsk::lane_id() == 0) heavy[0] = 1;
   __shared__ uint32_t part[11][4];
   const int w = threadIdx.x >> 6;
 #pragma unroll
@@ -1153,8 +1160,19 @@ extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long
   hipStream_t st = (hipStream_t)stream;
   LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
   if (n <= 1) return 0;
-  key_levels_kernel<<<lsk_blocks(n, 256, kLevelsBlocks), 256, 0, st>>>(keys, n, counts);
+  key_levels_kernel<<<lsk_blocks(n, 256, kLevelsBlocks), 256, 0, st>>>(keys, n, counts, 0, nullptr);
   LSK_CHECK_LAUNCH("key_levels");
+  return 0;
+}
+
+extern "C" int lsk_hip_key_census(const uint32_t *keys, int64_t n, unsigned long long *counts, int64_t run,
+                                  int32_t *heavy, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
+  LSK_HIP(hipMemsetAsync(heavy, 0, sizeof(int32_t), st));
+  if (n <= 1) return 0;
+  key_levels_kernel<<<lsk_blocks(n, 256, kLevelsBlocks), 256, 0, st>>>(keys, n, counts, run, heavy);
+  LSK_CHECK_LAUNCH("key_census");
   return 0;
 }
 

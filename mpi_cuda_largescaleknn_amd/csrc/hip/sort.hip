@@ -144,7 +144,8 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(
       const int e = w * (lsk::kWave * kRows) + r * lsk::kWave + lane;
       const bool valid = e < tn;
       kr[r] = valid ? kin[tb + e] : 0u;
-      vr[r] = valid ? vin[tb + e] : 0u;
+      // vin == NULL (the first pass of lsk_hip_sort_keys_iota): the value is the index
+      vr[r] = valid ? (vin ? vin[tb + e] : (uint32_t)(tb + e)) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
@@ -208,9 +209,8 @@ extern "C" size_t lsk_hip_sort_ws_bytes(int64_t n) {
   return (size_t)kRadix * sort_blocks(n) * sizeof(uint32_t) + 256;
 }
 
-extern "C" int lsk_hip_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt,
-                                  uint32_t *vals_alt, int64_t n, int key_bits, void *ws,
-                                  int *result_in_alt, void *stream) {
+static int sort_impl(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, int64_t n,
+                     int key_bits, void *ws, int *result_in_alt, bool iota, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   *result_in_alt = 0;
   if (n <= 1 || key_bits <= 0) return 0;
@@ -227,11 +227,29 @@ extern "C" int lsk_hip_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys
     LSK_CHECK_LAUNCH("sort_upsweep");
     scan_kernel<<<1, 1024, 0, s>>>(counts, (int64_t)kRadix * nb);
     LSK_CHECK_LAUNCH("sort_scan");
-    downsweep_kernel<<<nb, kThreads, 0, s>>>(ki, vi, ko, vo, n, shift, counts);
+    downsweep_kernel<<<nb, kThreads, 0, s>>>(ki, (iota && passes == 0) ? nullptr : vi, ko, vo, n, shift, counts);
     LSK_CHECK_LAUNCH("sort_downsweep");
     std::swap(ki, ko);
     std::swap(vi, vo);
   }
   *result_in_alt = passes & 1;
   return 0;
+}
+
+extern "C" int lsk_hip_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                                  int64_t n, int key_bits, void *ws, int *result_in_alt, void *stream) {
+  return sort_impl(keys, vals, keys_alt, vals_alt, n, key_bits, ws, result_in_alt, false, stream);
+}
+
+// As lsk_hip_sort_pairs with the values 0..n-1 generated by the first pass (vals is only
+// a ping-pong buffer: its contents are not read) — no iota array to write and read back.
+extern "C" int lsk_hip_sort_keys_iota(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                                      int64_t n, int key_bits, void *ws, int *result_in_alt, void *stream) {
+  if (n == 1) {  // (no pass runs: the single value must still be written)
+    hipStream_t s = (hipStream_t)stream;
+    LSK_HIP(hipMemsetAsync(vals, 0, sizeof(uint32_t), s));
+    *result_in_alt = 0;
+    return 0;
+  }
+  return sort_impl(keys, vals, keys_alt, vals_alt, n, key_bits, ws, result_in_alt, true, stream);
 }

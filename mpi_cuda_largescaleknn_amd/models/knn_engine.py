@@ -144,14 +144,22 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     n = points.shape[0]
     if box is None:
         box = K.bounds(points)
-    keys, iota = keys if keys is not None else K.morton(points, box)
-    skeys, perm = K.sort_pairs(keys, iota, 30)
-    perm = refine_heavy_cells(points, skeys, perm)
+    gpu = K.is_gpu(points)
+    if keys is not None:
+        skeys, perm = K.sort_pairs(keys[0], keys[1], 30)
+    elif gpu:  # (the sort's first pass generates the values: no iota array)
+        skeys, perm = K.sort_keys_iota(K.morton(points, box, with_iota=False)[0], 30)
+    else:
+        skeys, perm = K.sort_pairs(*K.morton(points, box), 30)
+    # level census (grid) and over-full-cell flag (refinement) in one pass over the keys
+    census = K.key_census(skeys[:n], HEAVY_RUN) if gpu and n > 1 else None
+    perm = refine_heavy_cells(points, skeys, perm, heavy=census[1] if census is not None else None)
     pts = K.gather3(points, perm, pad=K.PAD_POINTS)
     nodes, qnodes, depth = K.build_tree(pts, n)
     index = LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
     if grid:
-        index.grid = build_grid(index, skeys, density_n, grid_level)
+        index.grid = build_grid(index, skeys, density_n, grid_level,
+                                counts=census[0] if census is not None else None)
     return index
 
 
@@ -202,7 +210,7 @@ def grid_applies(distinct: list[int], n: int, g: int) -> bool:
 
 
 def build_grid(index: LocalIndex, skeys: torch.Tensor, density_n: int | None = None,
-               level: int | None = None) -> GridIndex | None:
+               level: int | None = None, counts: torch.Tensor | None = None) -> GridIndex | None:
     """Cell grid over index's sorted points (knn_grid.hip), or None (CPU, GRID=off).
 
     The level comes from the point counts (grid_level_for); whether the grid applies is
@@ -218,7 +226,8 @@ def build_grid(index: LocalIndex, skeys: torch.Tensor, density_n: int | None = N
     slots = K.grid_build(index.pts, skeys, n, index.box, g - 2)
     gate = None
     if GRID == "auto":
-        counts = K.key_levels_dev(skeys[:n])
+        if counts is None:
+            counts = K.key_levels_dev(skeys[:n])
         sq = K.grid_sq_dev(slots)
         gate = K.grid_decide(counts, sq, n, g, GRID_CROWD, True)
     return GridIndex(slots, g - 2, index.box, gate=gate)
@@ -260,7 +269,8 @@ def deferred_heavy_cells(clear: bool = False) -> bool:
     return hit
 
 
-def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Tensor,
+                       heavy: torch.Tensor | None = None) -> torch.Tensor:
     """Order inside over-full key cells (docs/ARCHITECTURE.md §2a).
 
     Keys have 10 bits per axis of the global cube, so a cluster much smaller than one
@@ -270,12 +280,12 @@ def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Te
     bounding box and re-sorted by (run, local key) with the same radix sort; only the
     order changes (results are exact in any order). Eager: one compare pass + one host
     sync, then work and memory proportional to the over-full runs only. Inside a HIP
-    graph capture: see REFINE_CAPTURE."""
+    graph capture: see REFINE_CAPTURE. `heavy`: the flag computed already (key_census)."""
     global LAST_REFINED
     n = skeys.shape[0]
     if n <= HEAVY_RUN:
         return perm
-    heavy_any = (skeys[HEAVY_RUN:] == skeys[:-HEAVY_RUN]).any()
+    heavy_any = heavy[0] != 0 if heavy is not None else (skeys[HEAVY_RUN:] == skeys[:-HEAVY_RUN]).any()
     if K.is_gpu(skeys) and torch.cuda.is_current_stream_capturing():
         if REFINE_CAPTURE:
             return _refine_all_cells(points, skeys, perm)

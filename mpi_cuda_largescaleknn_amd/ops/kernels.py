@@ -124,6 +124,33 @@ def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, key_bits: int = 30):
     return (ka, va) if alt.value else (keys, vals)
 
 
+def sort_keys_iota(keys: torch.Tensor, key_bits: int = 30):
+    """sort_pairs(keys, arange(n)) without the arange: the GPU sort's first pass generates
+    the values (no 4-byte-per-point array written and read back)."""
+    n = keys.shape[0]
+    if not is_gpu(keys):
+        return sort_pairs(keys, torch.arange(n, dtype=torch.int32), key_bits)
+    lib = _native.hip()
+    vals = torch.empty_like(keys)
+    ka = torch.empty_like(keys)
+    va = torch.empty_like(keys)
+    ws = torch.empty(lib.lsk_hip_sort_ws_bytes(n), dtype=torch.uint8, device=keys.device)
+    alt = C.c_int(0)
+    check(lib.lsk_hip_sort_keys_iota(_ptr(keys), _ptr(vals), _ptr(ka), _ptr(va), n, key_bits, _ptr(ws),
+                                     C.byref(alt), _stream(keys)), "sort_keys_iota")
+    return (ka, va) if alt.value else (keys, vals)
+
+
+def key_census(skeys: torch.Tensor, run: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """One device pass over sorted keys: (int64 [11] level counts as key_levels_dev, int32
+    [1] heavy flag: some key equals the one `run` positions earlier). No host read."""
+    cnt = torch.empty(11, dtype=torch.int64, device=skeys.device)
+    heavy = torch.empty(1, dtype=torch.int32, device=skeys.device)
+    check(_native.hip().lsk_hip_key_census(_ptr(skeys), skeys.shape[0], _ptr(cnt), int(run), _ptr(heavy),
+                                           _stream(skeys)), "key_census")
+    return cnt, heavy
+
+
 def segment_bounds(p: torch.Tensor, seg: torch.Tensor, nseg: int):
     """Per-segment AABB of GPU points p [m,3] with contiguous segment ids seg (int32,
     non-decreasing runs) -> (lo, hi) [nseg, 3]."""

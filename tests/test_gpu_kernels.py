@@ -62,6 +62,33 @@ def test_radix_sort_matches_torch_stable_sort(n, bits):
     assert torch.equal(vs.cpu(), vr)  # stability
 
 
+@pytest.mark.parametrize("n", [1, 2, 4097, 1000003])
+@pytest.mark.parametrize("bits", [8, 30])
+def test_sort_keys_iota_equals_sort_pairs(n, bits):
+    """The first pass generates the values 0..n-1 (no iota array): same result."""
+    g = torch.Generator().manual_seed(n + bits)
+    keys = torch.randint(0, 1 << bits, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    ks, vs = K.sort_keys_iota(keys.to(DEV).clone(), bits)
+    kr, vr = K.sort_pairs(keys, torch.arange(n, dtype=torch.int32), bits)
+    assert torch.equal(ks.cpu(), kr) and torch.equal(vs.cpu(), vr)
+
+
+@pytest.mark.parametrize("heavy", [False, True])
+def test_key_census_counts_and_heavy_flag(heavy):
+    """key_census = key_levels + the over-full-cell flag of refine_heavy_cells, one pass."""
+    n = 300_000
+    g = torch.Generator().manual_seed(7)
+    keys = torch.randint(0, 1 << 30, (n,), generator=g, dtype=torch.int64)
+    if heavy:
+        keys[1000:1000 + E.HEAVY_RUN + 5] = 12345
+    keys = torch.sort(keys).values.to(torch.int32)
+    counts, flag = K.key_census(keys.to(DEV), E.HEAVY_RUN)
+    lv = K.key_levels(keys.to(DEV))
+    assert [1] + [int(c) + 1 for c in counts.cpu().tolist()[1:]] == lv
+    ref = bool((keys[E.HEAVY_RUN:] == keys[:-E.HEAVY_RUN]).any())
+    assert bool(flag.item()) == ref == heavy
+
+
 def test_radix_sort_full_32bit_keys():
     n = 300000
     g = torch.Generator().manual_seed(5)
