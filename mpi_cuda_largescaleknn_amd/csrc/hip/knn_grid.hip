@@ -611,6 +611,13 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
 // one scan of all points when the tree is small, else the wave hands its unresolved
 // queries to the exact backstop (returns false).
 constexpr uint32_t kMaxCells = 4096;
+// Candidate budget of a wave, checked before each pass: max(kEvalBudget, kEvalsPerK * k),
+// ~80x a uniform wave at k = 100 (~3.4K). Beyond it the wave's unresolved queries go to
+// the exact backstop (one wave per query, 64 candidates per step) instead of one wave
+// streaming a dense cluster pass after pass (the grid is only chosen for near-uniform
+// data; GRID=on forces it). A check per cell instead cost 16 B/lane more scratch.
+constexpr uint32_t kEvalBudget = 1u << 18;
+constexpr uint32_t kEvalsPerK = 2048;
 constexpr uint32_t kScanAll = 1u << 16;
 
 template <int MODE>
@@ -709,7 +716,7 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
                                           oz + ((uint32_t)b >> 4));
             if (have) {
               process_cell<MODE>(s, G, pend, r2);
-              if (MODE == MODE_HIST) r2 = cull_r2<MODE>(s, G);
+                    if (MODE == MODE_HIST) r2 = cull_r2<MODE>(s, G);
               if (fbits(r2) == 0u) return true;
             }
             pend = c;
@@ -866,8 +873,8 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
 #pragma unroll 4
       for (int j = 0; j < kPool / lsk::kWave; j++) pool[j * lsk::kWave + lane] = 0u;
       if (kPool % lsk::kWave != 0 && lane < kPool % lsk::kWave) pool[kPool - kPool % lsk::kWave + lane] = 0u;
-      if (!grid_pass<MODE_HIST>(s, G, ntree)) {
-        gfail = true;
+      if (!grid_pass<MODE_HIST>(s, G, ntree) || G.evals > max(kEvalBudget, kEvalsPerK * k)) {
+        gfail = true;  // (a range the grid cannot serve, or over the wave's candidate budget)
         break;
       }
       bool ovf = false;
@@ -939,7 +946,7 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
     if (s.state != ST_READY) s.band_lo = s.band_w = 0;
     s.coff = pool_off;
     s.ccnt = 0;
-    if (!grid_pass<MODE_COLLECT>(s, G, ntree)) gfail = true;
+    if (G.evals > max(kEvalBudget, kEvalsPerK * k) || !grid_pass<MODE_COLLECT>(s, G, ntree)) gfail = true;
     if (!gfail && s.state == ST_READY) {
       qs |= QS_COLLECTED;
       if (s.ccnt != s.bc) qs |= QS_MISMATCH | QS_FAIL;

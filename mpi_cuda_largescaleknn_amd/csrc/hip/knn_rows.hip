@@ -123,6 +123,14 @@ constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(l
 constexpr uint32_t kShift0 = 20;
 constexpr uint32_t kMaxPasses = 96;
 constexpr uint32_t kGuardRounds = 1u << 22;
+// Step budget of a wave (all passes): max(kStepBudget, kStepsPerK * k) row-steps, ~16x
+// what a uniform wave takes at k = 100 (~500). A wave beyond it hands its unresolved
+// queries to the exact backstop, which runs one wave per query with 64 candidates per
+// step: queries next to a dense core far below their own scale (mixed_scale) would
+// otherwise stream millions of candidates through ONE wave, pass after pass, while the
+// rest of the GPU idles (2e7 points, k = 100: 0.26 s for the whole set).
+constexpr uint32_t kStepBudget = 8192;
+constexpr uint32_t kStepsPerK = 64;
 
 // LSK_PROFILE builds (tuning only) accumulate per-wave shader-clock cycles per activity
 // into stats[16..23]: proc hist, proc collect, traverse hist, traverse collect, replay
@@ -407,7 +415,8 @@ struct WaveCtx {
   uint32_t *logq, *logm;
   const float *p0, *p1, *pdef;  // tree point arrays (pdef: one that is non-empty)
   uint32_t n0, n1;
-  uint32_t guard;  // watchdog trips of the walk (never expected; see traverse)
+  uint32_t guard;  // bit 0: watchdog trip of the walk (never expected; see traverse);
+                   // bit 1: the wave's step budget ran out (kStepBudget)
 #ifdef LSK_PROFILE
   uint64_t prof[8];
   uint32_t prof_rows_entry, prof_rows_in;  // pass-1 row-steps with an entry / with a value in range
@@ -488,6 +497,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
     s.pband = false;
 #endif
     const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.trash, W.k, W.crowd);
+    if (W.steps >= max(kStepBudget, kStepsPerK * W.k)) W.guard |= 2u;
 #ifdef LSK_PROFILE
     if (MODE == MODE_HIST) {
       const uint32_t re = row_bits(__ballot(ccnt > 0u)), ri = row_bits(__ballot(lin));
@@ -505,7 +515,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
       if (dead && hcur < 512u && (uint32_t)(W.lane & 15) == (hcur >> 5))
         W.dead[hcur >> 9] |= 1u << (hcur & 31u);  // (index 0: dynamic, so it stays in scratch)
     }
-    if (MODE == MODE_HIST && W.crowd) break;  // crowded bin: the pass restarts narrower
+    if ((MODE == MODE_HIST && W.crowd) || W.guard) break;  // crowded bin: the pass restarts narrower
   }
   W.hd0 = min(W.hd0 + n, W.len0);
   W.hd1 = min(W.hd1 + n, W.len1);
@@ -955,7 +965,7 @@ __device__ __forceinline__ void traverse(Lane &s, WaveCtx &W, const lsk_knn_args
     LSK_PT(tp0);
     process_steps<MODE, NT>(s, W, A, nsteps);
     LSK_PADD(W.prof[MODE], tp0);
-    if (MODE == MODE_HIST && W.crowd) break;  // aborted pass (the caller restarts it)
+    if ((MODE == MODE_HIST && W.crowd) || W.guard) break;  // aborted pass (the caller restarts it)
   }
 }
 
@@ -1357,7 +1367,9 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     LSK_PADD(W.prof[6], ts0);
   }
 
-  // a truncated walk (watchdog) invalidates the whole wave; tests can force failures
+  // a truncated walk (watchdog or step budget: every later pass stops at once, so its
+  // decisions may rest on partial counts) invalidates the whole wave; tests can force
+  // failures
   if (W.guard) qs |= QS_FAIL;
   if (A.debug_fail_mod > 0 && qi % A.debug_fail_mod == 0) qs |= QS_FAIL;
   const bool failed = valid && (qs & QS_FAIL);
