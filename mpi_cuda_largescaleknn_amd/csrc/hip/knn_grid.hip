@@ -1172,11 +1172,11 @@ extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long
   return 0;
 }
 
+// (counts and heavy are zeroed by the caller: tiny hipMemsetAsync nodes in a captured HIP
+// graph were seen not to re-zero them on later replays — ROCm 7.0, 88 and 4 bytes)
 extern "C" int lsk_hip_key_census(const uint32_t *keys, int64_t n, unsigned long long *counts, int64_t run,
                                   int32_t *heavy, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
-  LSK_HIP(hipMemsetAsync(heavy, 0, sizeof(int32_t), st));
   if (n <= 1) return 0;
   key_levels_kernel<<<lsk_blocks(n, 256, kLevelsBlocks), 256, 0, st>>>(keys, n, counts, run, heavy);
   LSK_CHECK_LAUNCH("key_census");
@@ -1185,7 +1185,6 @@ extern "C" int lsk_hip_key_census(const uint32_t *keys, int64_t n, unsigned long
 
 extern "C" int lsk_hip_grid_sq(const uint32_t *slots, int64_t nslot, unsigned long long *out, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  LSK_HIP(hipMemsetAsync(out, 0, sizeof(unsigned long long), st));
   if (nslot <= 0) return 0;
   grid_sq_kernel<<<lsk_blocks(nslot, 256, kLevelsBlocks), 256, 0, st>>>((const uint4 *)slots, nslot, out);
   LSK_CHECK_LAUNCH("grid_sq");

@@ -78,11 +78,21 @@ class GridIndex:
     inf4: torch.Tensor | None = None  # 4 x +inf on the device (candidate padding)
     gate: torch.Tensor | None = None  # device int32 [1]: 1 = the grid applies (decided on
                                       # the device, GRID=auto), None = always (GRID=on)
+    census: tuple | None = None       # (level counts, crowding sum) the gate came from
 
     def view(self) -> tuple:
         if self.inf4 is None:
             self.inf4 = torch.full((4,), math.inf, dtype=torch.float32, device=self.slots.device)
         return (self.slots, self.level, self.box, self.inf4, self.gate)
+
+    def decision(self) -> dict:
+        """Host read of what the device decided from (debugging / reporting)."""
+        out = {"level": self.level + 2, "applies": self.applies()}
+        if self.census is not None:
+            c = [int(x) for x in self.census[0].cpu().tolist()]
+            out.update(distinct_g=c[self.level + 2] + 1, distinct_g1=c[self.level + 1] + 1,
+                       crowd_sum=int(self.census[1].item()))
+        return out
 
     def applies(self) -> bool:
         """Host read of the device decision (reporting only; never on the hot path)."""
@@ -230,7 +240,10 @@ def build_grid(index: LocalIndex, skeys: torch.Tensor, density_n: int | None = N
             counts = K.key_levels_dev(skeys[:n])
         sq = K.grid_sq_dev(slots)
         gate = K.grid_decide(counts, sq, n, g, GRID_CROWD, True)
-    return GridIndex(slots, g - 2, index.box, gate=gate)
+        census = (counts, sq)
+    else:
+        census = None
+    return GridIndex(slots, g - 2, index.box, gate=gate, census=census)
 
 
 HEAVY_RUN = 4096  # sorted points sharing one 30-bit key that trigger a second-level key
@@ -462,6 +475,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     if len(trees) == 1 and init_d2 is None:  # (a local pass, not a halo re-query)
         if use_grid and index.grid.gate is not None:
             GATES_SEEN.append(index.grid.gate)  # grid or rows: resolved by kernels_used()
+            GRIDS_SEEN[:] = [index.grid]  # (the last one: debugging)
             del GATES_SEEN[:-1024]  # (reporting only: a long stream keeps the last sets)
         else:
             KERNELS_USED.add("grid" if use_grid else impl)
@@ -505,6 +519,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
 # gate in GATES_SEEN; kernels_used() reads them (a host read: after the timed region).
 KERNELS_USED: set = set()
 GATES_SEEN: list = []
+GRIDS_SEEN: list = []
 
 
 def kernels_used() -> list:

@@ -144,8 +144,8 @@ def sort_keys_iota(keys: torch.Tensor, key_bits: int = 30):
 def key_census(skeys: torch.Tensor, run: int) -> tuple[torch.Tensor, torch.Tensor]:
     """One device pass over sorted keys: (int64 [11] level counts as key_levels_dev, int32
     [1] heavy flag: some key equals the one `run` positions earlier). No host read."""
-    cnt = torch.empty(11, dtype=torch.int64, device=skeys.device)
-    heavy = torch.empty(1, dtype=torch.int32, device=skeys.device)
+    cnt = torch.zeros(11, dtype=torch.int64, device=skeys.device)
+    heavy = torch.zeros(1, dtype=torch.int32, device=skeys.device)
     check(_native.hip().lsk_hip_key_census(_ptr(skeys), skeys.shape[0], _ptr(cnt), int(run), _ptr(heavy),
                                            _stream(skeys)), "key_census")
     return cnt, heavy
@@ -445,7 +445,7 @@ def key_levels_dev(skeys: torch.Tensor) -> torch.Tensor:
 
 def grid_sq_dev(slots: torch.Tensor) -> torch.Tensor:
     """grid_sq without the host read: int64 [1] on the device."""
-    out = torch.empty(1, dtype=torch.int64, device=slots.device)
+    out = torch.zeros(1, dtype=torch.int64, device=slots.device)
     check(_native.hip().lsk_hip_grid_sq(_ptr(slots), slots.shape[0], _ptr(out), _stream(slots)), "grid_sq")
     return out
 
@@ -460,7 +460,7 @@ def grid_decide(counts: torch.Tensor, sq: torch.Tensor, n: int, g: int, crowd: f
 
 def grid_sq(slots: torch.Tensor) -> int:
     """Sum over grid slots of population^2 (host read)."""
-    out = torch.empty(1, dtype=torch.int64, device=slots.device)
+    out = torch.zeros(1, dtype=torch.int64, device=slots.device)
     check(_native.hip().lsk_hip_grid_sq(_ptr(slots), slots.shape[0], _ptr(out), _stream(slots)), "grid_sq")
     return int(out.item())
 

@@ -581,8 +581,9 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         ev_pub.record(comp)
         cur.wait_event(ev_pub)  # (the hook's collectives follow the publish)
     pend: list = []
-    d2 = torch.zeros(n, dtype=torch.float32, device=index.device)  # interior groups: radius 0 below
     with ctx:
+        # (allocated and zeroed on the compute stream: the passes below write it there)
+        d2 = torch.zeros(n, dtype=torch.float32, device=index.device)  # interior groups: radius 0 below
         # 2. the boundary groups' local pass first: their exact radii (interior leaves 0)
         #    are what the other ranks filter their points with
         E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=blist, ngroups=ng,

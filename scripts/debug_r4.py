@@ -1,0 +1,91 @@
+"""Round-4 debugging aid: the device grid gate (eager vs graph capture) and the
+boundary-first halo on loopback ranks against one rank (mismatch census)."""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+from datasets import uniform  # noqa: E402
+from mpi_cuda_largescaleknn_amd.models import knn_engine as E  # noqa: E402
+from mpi_cuda_largescaleknn_amd.ops import kernels as K  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel.comm import run_loopback  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def gate_report(tag, idx):
+    g = idx.grid
+    print(tag, "level", g.level + 2, "gate", None if g.gate is None else int(g.gate.item()), flush=True)
+
+
+n = 150_000
+p = uniform(n, seed=1).to(DEV)
+idx = E.build_index(p, grid=True)
+gate_report("eager", idx)
+skeys = K.morton(idx.pts[:n], idx.box, with_iota=False)[0]
+skeys = torch.sort(skeys.long() & 0x3FFFFFFF).values.to(torch.int32)
+cnt, hv = K.key_census(skeys, E.HEAVY_RUN)
+print("census", cnt.cpu().tolist(), "heavy", int(hv.item()), "key_levels", K.key_levels(skeys), flush=True)
+sq = K.grid_sq_dev(idx.grid.slots)
+print("sq", int(sq.item()), "sq/n", int(sq.item()) / n, flush=True)
+
+side = torch.cuda.Stream(DEV)
+side.wait_stream(torch.cuda.current_stream(DEV))
+keep = {}
+with torch.cuda.stream(side):
+    keep["i"] = E.build_index(p, grid=True)
+torch.cuda.current_stream(DEV).wait_stream(side)
+torch.cuda.synchronize()
+gate_report("side-stream eager", keep["i"])
+gr = torch.cuda.CUDAGraph()
+with torch.cuda.graph(gr):
+    keep["c"] = E.build_index(p, grid=True)
+torch.cuda.synchronize()
+gr.replay()
+torch.cuda.synchronize()
+gate_report("captured+replayed", keep["c"])
+
+# the graph test's body: the captured unordered pipeline replayed on new data
+from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm  # noqa: E402
+from datasets import clustered  # noqa: E402
+n = 150_000
+host_pts = torch.empty((n, 3), dtype=torch.float32, pin_memory=True)
+host_out = torch.empty(n, dtype=torch.float32, pin_memory=True)
+host_pts.copy_(uniform(n, seed=1))
+comm = SingleComm(DEV)
+cfg = E.KnnConfig(k=100)
+
+
+def body():
+    pts = host_pts.to(DEV, non_blocking=True)
+    out = PL.unordered_knn(pts, comm, cfg, n_total=n, out=host_out)
+    if out.data_ptr() != host_out.data_ptr():
+        host_out.copy_(out, non_blocking=True)
+
+
+side = torch.cuda.Stream(DEV)
+side.wait_stream(torch.cuda.current_stream(DEV))
+with torch.cuda.stream(side):
+    body()
+torch.cuda.current_stream(DEV).wait_stream(side)
+torch.cuda.synchronize()
+print("warmup gates", [int(x.item()) for x in E.GATES_SEEN], flush=True)
+E.reset_kernels_used()
+gr2 = torch.cuda.CUDAGraph()
+with torch.cuda.graph(gr2):
+    body()
+torch.cuda.synchronize()
+print("captured gates", len(E.GATES_SEEN), flush=True)
+G = E.GRIDS_SEEN[0]
+for name, data in (("u1", uniform(n, seed=1)), ("cl", clustered(n, seed=2)), ("u3", uniform(n, seed=3) * 7.0 - 2.0)):
+    host_pts.copy_(data)
+    gr2.replay()
+    torch.cuda.synchronize()
+    ok = torch.equal(host_out, E.knn_distances(data.to(DEV), 100).cpu())
+    print("replay", name, "gate", int(E.GATES_SEEN[0].item()), "equal", ok, G.decision(), flush=True)
+    eg = E.build_index(data.to(DEV), grid=True)
+    print("   eager", eg.grid.decision(), flush=True)
+torch.cuda.empty_cache()
+

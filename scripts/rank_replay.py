@@ -137,6 +137,7 @@ for r in range(P):
            "local_ms": round(t_local, 2), "halo_ms": round(t_mask + t_htree, 2), "requery_ms": round(t_req, 2),
            "return_ms": round(t_ret, 2)}
     row["total_ms"] = round(sum(v for kk, v in row.items() if kk.endswith("_ms")), 2)
+    row["grid"] = index.grid.decision() if index.grid is not None else None
     rows.append(row)
     print(json.dumps(row), flush=True)
     del index, hidx, ub, fl, d2, fin, mask, res, perm
