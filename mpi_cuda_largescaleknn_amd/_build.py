@@ -46,7 +46,8 @@ def _sources(sub: str, ext: str) -> list[str]:
 
 
 def _headers() -> list[str]:
-    return sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True))
+    return sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) +
+                  glob.glob(os.path.join(CSRC, "**", "*.inc"), recursive=True))
 
 
 def _stale(target: str, deps: list[str]) -> bool:

@@ -610,6 +610,7 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
 // the local spacing: k beyond the local point count, or an estimate far off) is served by
 // one scan of all points when the tree is small, else the wave hands its unresolved
 // queries to the exact backstop (returns false).
+constexpr unsigned kStrideBlocks = 1024;  // persistent form: 2048 waves, 2 per SIMD
 constexpr uint32_t kMaxCells = 4096;
 // Candidate budget of a wave, checked before each pass: max(kEvalBudget, kEvalsPerK * k),
 // ~80x a uniform wave at k = 100 (~3.4K). Beyond it the wave's unresolved queries go to
@@ -728,299 +729,26 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
   return true;
 }
 
+// STRIDE = false: one wave per group (the normal launch). STRIDE = true: a small persistent
+// grid strides over the groups — the form launched when the device gate is expected to
+// pick knn_rows: every wave returns at once when it does, instead of millions of blocks
+// each being dispatched only to return (1B points: ~16 ms per launch).
+template <bool STRIDE>
 __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
   __shared__ uint32_t lds[kWPB][kPool + 8 * kCullGroups];
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
-  const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
-  const uint64_t wave = (uint64_t)blk * kWPB + wid;
-  const uint64_t ngroups = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
-  if (wave >= ngroups) return;
-  if (A.groups && A.ngroups_dev && wave >= (uint64_t)*A.ngroups_dev) return;
-  if (A.gate && *A.gate != A.gate_on) return;  // the device chose knn_rows
-  // a listed group (the boundary / interior passes of a distributed run) or the wave's own
-  const uint32_t grp = lsk::uniform(A.groups ? A.groups[wave] : (uint32_t)wave);
-  const int64_t q0 = (int64_t)grp * lsk::kBucket;
-  const int64_t qi = q0 + lane;
-  const bool valid = qi < A.nq;
-  const uint32_t nvalid = (uint32_t)((A.nq - q0) < lsk::kBucket ? (A.nq - q0) : lsk::kBucket);
-  const uint32_t k = (uint32_t)A.k;
-  uint32_t *pool = lds[wid];
-
-  GridCtx G;
-  G.pts = A.tree[0].pts;
-  G.inf4 = V.inf4;
-  G.slots = (const uint4 *)V.slots;
-  {
-    const lsk::cfloat_p bx = lsk::as_const(V.box);
-    G.ox = bx[0];
-    G.oy = bx[1];
-    G.oz = bx[2];
-    G.scale = bx[6];
-    const float ext = bx[7];
-    G.step = ext * (1.f / 1024.f);
-    const float mag = fmaxf(fmaxf(fabsf(G.ox), fabsf(G.oy)), fmaxf(fabsf(G.oz), 0.f)) + ext;
-    G.eps = mag * 0x1p-19f;
-  }
-  G.lc = (uint32_t)V.level;
-  G.pool = pool;
-  G.lane = lane;
-  G.rbox = (float *)(pool + kPool);
-  G.trash = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u + (uint32_t)kBins * 128u;
-  asm volatile("" : "+v"(G.trash));
-  G.k = k;
-  G.evals = G.cells_n = G.segs = 0;
-#ifdef LSK_GRID_PROFILE
-  for (int i = 0; i < 8; i++) G.prof[i] = 0;
-  G.ev_mode[0] = G.ev_mode[1] = 0;
-  LSK_GT(twave0);
-#endif
-
-  Lane s;
-  s.qx = valid ? A.qpts[3 * qi] : 0.f;
-  s.qy = valid ? A.qpts[3 * qi + 1] : 0.f;
-  s.qz = valid ? A.qpts[3 * qi + 2] : 0.f;
-  uint32_t qs = 0;
-  const float inf = __builtin_inff();
-  G.wlx = lsk::wave_min(valid ? s.qx : inf);
-  G.whx = lsk::wave_max(valid ? s.qx : -inf);
-  G.wly = lsk::wave_min(valid ? s.qy : inf);
-  G.why = lsk::wave_max(valid ? s.qy : -inf);
-  G.wlz = lsk::wave_min(valid ? s.qz : inf);
-  G.whz = lsk::wave_max(valid ? s.qz : -inf);
-  {
-    // per-row boxes (an empty row: +inf / -inf, never needs anything)
-    const float q3[3] = {s.qx, s.qy, s.qz};
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-      const float lo = group_min(valid ? q3[a] : inf), hi = group_max(valid ? q3[a] : -inf);
-      if ((lane & (kCullLanes - 1)) == a) G.rbox[(lane / kCullLanes) * 8 + a] = lo;
-      if ((lane & (kCullLanes - 1)) == 3 + a) G.rbox[(lane / kCullLanes) * 8 + 3 + a] = hi;
-    }
-  }
-
-  bool dup;
-  float r_est2 = own_group_estimate(s, nvalid, k, dup);
-  if (valid && !dup) {
-    const int64_t nb = lane == 0 ? qi - 1 : (lane == (int)nvalid - 1 ? qi + 1 : -1);
-    if (nb >= 0 && nb < A.nq)
-      dup = A.qpts[3 * nb] == s.qx && A.qpts[3 * nb + 1] == s.qy && A.qpts[3 * nb + 2] == s.qz;
-  }
-  const bool zero_est = valid && (dup || r_est2 == 0.f);
-  {
-    const bool ok = valid && r_est2 > 0.f && r_est2 < inf;
-    const uint32_t kq = max(1u, nvalid / 4u);
-    const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
-    if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
-    const uint32_t mb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, max(1u, nvalid / 2u));
-    if (ok && mb < lsk::kInfBits) r_est2 = sqrtf(r_est2 * bitsf(mb)) * kEstCalib;
-  }
-  if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
-    r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
-    qs |= QS_HINT;
-  }
-  if (!(r_est2 > 0.f) || !(r_est2 < inf)) r_est2 = 1.f;
-
-  const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
-  const uint32_t cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
-  s.band_lo = s.band_w = s.bc = s.coff = s.ccnt = 0;
-  s.lo_b = s.hi_b = s.shift = s.c_hi = 0;
-  s.bin_hi = 0;
-  s.c_base = 0;
-  s.nudf = 0;
-
-  uint32_t hist_passes = 0, limit = 0;
-  if (!valid || A.tree[0].n < (int64_t)k) {
-    s.state = ST_DONE;
-    s.hi_b = 0;
-    s.lo_b = cut_b;
-    qs |= QS_DONE_CUT;
+  if (!STRIDE) {
+    const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
+    const uint64_t wave = (uint64_t)blk * kWPB + wid;
+#include "knn_grid_wave.inc"
   } else {
-    s.state = ST_HIST;
-    const uint32_t est_b = fbits(r_est2);
-    const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;
-    const uint32_t lo0 = est_b > off ? est_b - off : 0u;
-    if (zero_est) {
-      set_range(s, 0u, 0u, cut_lim, kUnknown);
-      s.band_lo = lo0;
-      s.band_w = 1u;
-    } else {
-      set_range(s, lo0, kShift0, cut_lim, kUnknown);
-    }
-  }
-
-  uint32_t pool_off = 0;
-  uint32_t passes = 0;
-  bool gfail = false;
-  const uint32_t ntree = (uint32_t)A.tree[0].n;
-  for (;;) {
-    while (__ballot(s.state == ST_HIST)) {
-      if (++passes > kMaxPasses) {
-        limit = 1;
-        if (s.state != ST_DONE) {
-          s.state = ST_DONE;
-          s.lo_b = kNaNBits;
-          qs |= QS_LIMIT | QS_FAIL;
-        }
-        break;
-      }
-      hist_passes++;
-      if (s.state != ST_HIST) {
-        s.hi_b = 0;
-        s.c_hi = 0;
-        s.bin_hi = 0;
-      }
-#pragma unroll 4
-      for (int j = 0; j < kPool / lsk::kWave; j++) pool[j * lsk::kWave + lane] = 0u;
-      if (kPool % lsk::kWave != 0 && lane < kPool % lsk::kWave) pool[kPool - kPool % lsk::kWave + lane] = 0u;
-      if (!grid_pass<MODE_HIST>(s, G, ntree) || G.evals > max(kEvalBudget, kEvalsPerK * k)) {
-        gfail = true;  // (a range the grid cannot serve, or over the wave's candidate budget)
-        break;
-      }
-      bool ovf = false;
-      if (s.state == ST_HIST && !hist_consistent(s, pool, lane)) {
-        s.state = ST_DONE;
-        s.lo_b = kNaNBits;
-        qs |= QS_BINOVF | QS_FAIL;
-      }
-      if (s.state == ST_HIST) {
-        const uint32_t top = top_count(s, pool, lane);
-        if (s.c_hi < k) {
-          if (s.hi_b >= cut_lim) {
-            s.state = ST_DONE;
-            s.lo_b = cut_b;
-            qs |= QS_DONE_CUT;
-          } else {
-            ovf = true;
-            qs |= QS_OVERFLOW;
-            if (s.band_w != 0u && s.band_lo > s.hi_b) {
-              set_range(s, s.band_lo, kShift0, cut_lim, kUnknown);  // failed zero probe
-            } else {
-              set_range(s, s.hi_b, kShift0, cut_lim, s.c_hi);
-            }
-            s.band_lo = s.band_w = 0u;
-          }
-        } else if (s.bin_hi <= 1 && s.c_base == kUnknown) {
-          qs |= QS_UNDERFLOW;
-          underflow_restart(s);
-        } else {
-          const uint32_t below = s.bin_hi == 1 ? s.c_base : s.c_hi - top;
-          const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
-          const uint32_t bw = s.hi_b - bl;
-          if (bw <= 1u) {
-            s.state = ST_DONE;
-            s.lo_b = bl;
-            qs |= QS_DONE_BAND1;
-          } else {
-            s.state = ST_READY;
-            s.band_lo = bl;
-            s.band_w = bw;
-            s.c_base = below;
-            s.bc = s.c_hi - below;
-          }
-        }
-      }
-      (void)ovf;
-    }
-    if (limit || gfail) break;
-    const uint32_t need = s.state == ST_READY ? s.bc : 0u;
-    uint32_t x = need;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    const uint32_t total = __shfl(x, 63);
-    pool_off = x - need;
-    if (total <= (uint32_t)kPool) break;
-    if (s.state == ST_READY && s.bc > (uint32_t)(kPool / lsk::kWave)) {
-      qs |= QS_REFINE;
-      const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;
-      set_range(s, s.band_lo, sh, s.band_lo + s.band_w, s.c_base);
-      s.band_lo = s.band_w = 0;
-      s.state = ST_HIST;
-    }
-  }
-
-  if (!limit && !gfail && __ballot(s.state == ST_READY)) {
-    if (s.state != ST_READY) s.band_lo = s.band_w = 0;
-    s.coff = pool_off;
-    s.ccnt = 0;
-    if (G.evals > max(kEvalBudget, kEvalsPerK * k) || !grid_pass<MODE_COLLECT>(s, G, ntree)) gfail = true;
-    if (!gfail && s.state == ST_READY) {
-      qs |= QS_COLLECTED;
-      if (s.ccnt != s.bc) qs |= QS_MISMATCH | QS_FAIL;
-      uint32_t *h = pool + s.coff;
-      const uint32_t c = min(s.ccnt, s.bc), m = k - s.c_base;
-      if (!(qs & QS_FAIL) && m >= 1 && m <= c) {
-        for (int i = (int)(m / 2) - 1; i >= 0; i--) heap_sift(h, (uint32_t)i, m);
-        for (uint32_t i = m; i < c; i++) {
-          const uint32_t v = h[i];
-          if (v < h[0]) {
-            h[0] = v;
-            heap_sift(h, 0, m);
-          }
-        }
-        s.lo_b = h[0];
-      } else {
-        qs |= QS_MISMATCH | QS_FAIL;
-        s.lo_b = kNaNBits;
-      }
-    }
-  }
-
-  // a pass the grid could not serve: every unresolved query goes to the backstop
-  if (gfail && s.state != ST_DONE) qs |= QS_FAIL;
-  if (A.debug_fail_mod > 0 && qi % A.debug_fail_mod == 0) qs |= QS_FAIL;
-  const bool failed = valid && (qs & QS_FAIL);
-  if (failed) s.lo_b = kNaNBits;
-  if (A.fail_count) {
-    const uint64_t fm = __ballot(failed);
-    if (fm) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(A.fail_count, (uint32_t)__popcll(fm));
-      base = lsk::uniform(base);
-      const uint64_t slot = (uint64_t)base + (uint64_t)__popcll(fm & ((1ull << lane) - 1ull));
-      if (failed && slot < (uint64_t)A.fail_cap) A.fail_list[slot] = (uint32_t)qi;
-    }
-  }
-  if (valid) {
-    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.lo_b));
-    if (A.out_d2) A.out_d2[qi] = bitsf(s.lo_b);
-    if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
-  }
-#ifdef LSK_GRID_PROFILE
-  LSK_GADD(G.prof[7], twave0);
-  if (A.stats && lane == 0) {
-    // proc = processing; walk = pass total minus processing
-    atomicAdd(&A.stats[16], (unsigned long long)G.prof[0]);
-    atomicAdd(&A.stats[17], (unsigned long long)G.prof[1]);
-    atomicAdd(&A.stats[18], (unsigned long long)(G.prof[2] - G.prof[0]));
-    atomicAdd(&A.stats[19], (unsigned long long)(G.prof[3] - G.prof[1]));
-    atomicAdd(&A.stats[23], (unsigned long long)G.prof[7]);
-    atomicAdd(&A.stats[12], (unsigned long long)G.ev_mode[0]);
-    atomicAdd(&A.stats[13], (unsigned long long)G.ev_mode[1]);
-  }
-#endif
-  if (A.stats) {
-    auto cnt = [&](uint32_t bit) { return (unsigned long long)__popcll(__ballot(valid && (qs & bit))); };
-    const unsigned long long c_ovf = cnt(QS_OVERFLOW), c_udf = cnt(QS_UNDERFLOW), c_ref = cnt(QS_REFINE),
-                             c_mm = cnt(QS_MISMATCH), c_hint = cnt(QS_HINT), c_fail = cnt(QS_FAIL),
-                             c_bovf = cnt(QS_BINOVF);
-    if (lane == 0) {
-      atomicAdd(&A.stats[0], (unsigned long long)G.evals);  // candidates per lane
-      atomicAdd(&A.stats[1], (unsigned long long)G.cells_n);
-      atomicAdd(&A.stats[2], (unsigned long long)G.segs);
-      atomicAdd(&A.stats[3], (unsigned long long)hist_passes);
-      atomicAdd(&A.stats[4], c_ovf);
-      atomicAdd(&A.stats[5], c_udf);
-      atomicAdd(&A.stats[6], c_ref);
-      atomicAdd(&A.stats[7], c_mm);
-      atomicAdd(&A.stats[8], (unsigned long long)limit);
-      atomicAdd(&A.stats[10], 1ull);
-      atomicAdd(&A.stats[11], c_hint);
-      atomicAdd(&A.stats[26], c_fail);
-      atomicAdd(&A.stats[27], c_bovf);
+    if (A.gate && *A.gate != A.gate_on) return;
+    const uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+    for (uint64_t w = (uint64_t)blockIdx.x * kWPB + wid; w < nwaves; w += (uint64_t)gridDim.x * kWPB) {
+      [&](const uint64_t wave) {
+#include "knn_grid_wave.inc"
+      }(w);
     }
   }
 }
@@ -1205,7 +933,11 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
   }
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
-  knn_grid_kernel<<<lsk_blocks(ngroups, kWPB), kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+  const unsigned nblk = lsk_blocks(ngroups, kWPB);
+  if (A.pad2 == 1)  // persistent strided form (see knn_grid_kernel)
+    knn_grid_kernel<true><<<nblk < kStrideBlocks ? nblk : kStrideBlocks, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+  else
+    knn_grid_kernel<false><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
   LSK_CHECK_LAUNCH("knn_grid");
   return 0;
 }

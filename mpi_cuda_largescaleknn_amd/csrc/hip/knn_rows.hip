@@ -1040,402 +1040,27 @@ __device__ __forceinline__ bool hist_consistent(const Lane &s, const uint32_t *p
 }
 
 
-template <int RCAP, int NT>
+// STRIDE = false: one wave per group (the normal launch). STRIDE = true: a small persistent
+// grid strides over the groups — the form launched beside the grid kernel when the device
+// gate is expected to pick the grid: every wave returns at once when it does, instead of
+// millions of blocks each being dispatched only to return (1B points: ~16 ms per launch).
+template <int RCAP, int NT, bool STRIDE>
 __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_rows_kernel(const lsk_knn_args A) {
   __shared__ WaveLdsR<RCAP> lds[kWavesPerBlock];
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
-  const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
-  const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid;
-  const uint64_t ngroups = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
-  if (wave >= ngroups) return;
-  if (A.groups && A.ngroups_dev && wave >= (uint64_t)*A.ngroups_dev) return;
-  if (A.gate && *A.gate != A.gate_on) return;  // the device chose the grid kernel
-  const uint32_t g = lsk::uniform(A.groups ? A.groups[wave] : (uint32_t)wave);
-  const int64_t q0 = (int64_t)g * lsk::kBucket;
-  const int64_t qi = q0 + lane;
-  const bool valid = qi < A.nq;
-  const uint32_t nvalid = (uint32_t)((A.nq - q0) < lsk::kBucket ? (A.nq - q0) : lsk::kBucket);
-  const uint32_t k = (uint32_t)A.k;
-
-  WaveCtx W;
-  W.L = &lds[wid].w;
-  W.rl = lds[wid].rl;
-  W.rcap = RCAP;
-  W.lane = lane;
-  W.row = lane >> 4;
-  W.trash = lds_addr(W.L->pool) + ((uint32_t)lane & 31u) * 4u + (uint32_t)kBins * 128u;
-  asm volatile("" : "+v"(W.trash));
-  W.k = k;
-  W.g = g;
-  W.seed = A.seed;
-  W.len0 = W.len1 = W.len2 = W.len3 = W.rlen = 0;
-  W.hd0 = W.hd1 = W.hd2 = W.hd3 = W.rhead = 0;
-  uint32_t logq[kLogWords], logm[kLogWords];  // private (scratch) pass-1 log
-  W.logq = logq;
-  W.logm = logm;
-  uint32_t deadw[2];  // private dead-row-step stream word (WaveCtx::dead)
-  W.dead = deadw;
-  W.logn = 0;
-  W.logging = W.log_ok = false;
-  W.crowd = false;
-  W.p0 = A.tree[0].pts;
-  W.p1 = A.ntrees > 1 ? A.tree[1].pts : A.tree[0].pts;
-  W.n0 = A.ntrees > 0 ? (uint32_t)A.tree[0].n : 0u;
-  W.n1 = A.ntrees > 1 ? (uint32_t)A.tree[1].n : 0u;
-  W.pdef = W.n0 > 0 ? W.p0 : W.p1;
-  W.guard = 0;
-#ifdef LSK_PROFILE
-  for (int i = 0; i < 8; i++) W.prof[i] = 0;
-  W.prof_rows_entry = W.prof_rows_in = 0;
-  W.prof_crows_entry = W.prof_crows_in = 0;
-  LSK_PT(twave0);
-#endif
-  W.steps = W.quarters = W.nodes_visited = W.csteps = W.cnodes = 0;
-
-  Lane s;
-  s.qx = valid ? A.qpts[3 * qi] : 0.f;
-  s.qy = valid ? A.qpts[3 * qi + 1] : 0.f;
-  s.qz = valid ? A.qpts[3 * qi + 2] : 0.f;
-  uint32_t qs = 0;
-
-  const float inf = __builtin_inff();
-  const float lx = lsk::wave_min(valid ? s.qx : inf), hx = lsk::wave_max(valid ? s.qx : -inf);
-  const float ly = lsk::wave_min(valid ? s.qy : inf), hy = lsk::wave_max(valid ? s.qy : -inf);
-  const float lz = lsk::wave_min(valid ? s.qz : inf), hz = lsk::wave_max(valid ? s.qz : -inf);
-  W.cx = 0.5f * (lx + hx);
-  W.cy = 0.5f * (ly + hy);
-  W.cz = 0.5f * (lz + hz);
-  W.wlx = lx; W.wly = ly; W.wlz = lz;
-  W.whx = hx; W.why = hy; W.whz = hz;
-
-  bool dup;
-  float r_est2 = own_group_estimate(s, nvalid, k, dup);
-  if (valid && !dup) {
-    // copies sort next to each other: a copy at a group edge may sit in the next group
-    const int64_t nb = lane == 0 ? qi - 1 : (lane == (int)nvalid - 1 ? qi + 1 : -1);
-    if (nb >= 0 && nb < A.nq)
-      dup = A.qpts[3 * nb] == s.qx && A.qpts[3 * nb + 1] == s.qy && A.qpts[3 * nb + 2] == s.qz;
-  }
-  // an exact copy of the query inside its own group (or k = 1): start with a probe of
-  // the d² = 0 bin (zero probe below) instead of a range around a radius estimate — a
-  // point with >= k copies then costs ~k candidates instead of all its copies
-  const bool zero_est = valid && (dup || r_est2 == 0.f);
-  {
-    // Robust cap: a group straddling a Morton discontinuity has lanes with few
-    // same-side neighbours in the group, whose estimate is then orders of magnitude too
-    // large (range far above the k-th value: huge first-pass bound, one slow wave).
-    // Cap at 16x (4 octaves of d2) the wave's lower-quartile estimate.
-    const bool ok = valid && r_est2 > 0.f && r_est2 < inf;
-    const uint32_t kq = max(1u, nvalid / 4u);
-    const uint32_t pb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, kq);
-    if (pb < lsk::kInfBits) r_est2 = fminf(r_est2, 16.f * bitsf(pb));
-    // geometric blend with the wave median (the per-lane 8-NN estimate is noisy, the
-    // median alone misses density changes inside a group), calibrated so that the median
-    // of true/estimate is 1 on uniform and clustered data (offline study: the k-th lands
-    // below 2x the blend for 99.5 % of queries, vs 2.9x for the lane estimate)
-    const uint32_t mb = lsk::wave_kth_smallest(ok ? fbits(r_est2) : 0xffffffffu, max(1u, nvalid / 2u));
-    if (ok && mb < lsk::kInfBits) r_est2 = sqrtf(r_est2 * bitsf(mb)) * (float)LSK_EST_CALIB;
-  }
-  if (!(r_est2 > 0.f) || !(r_est2 < inf)) {
-    r_est2 = A.r_hint2 >= 0.f ? A.r_hint2 : A.tree[0].nodes[3];
-    qs |= QS_HINT;
-  }
-  if (!(r_est2 > 0.f) || !(r_est2 < inf)) r_est2 = 1.f;
-
-  const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
-  // cutoff bits: wave-uniform (an SGPR, not a per-lane field)
-  const uint32_t cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
-  s.band_lo = s.band_w = s.bc = s.coff = s.ccnt = 0;
-  // every lane's histogram state is defined (lanes that never histogram included:
-  // the wave-wide shrink step reads bin_hi / c_hi of all lanes)
-  s.lo_b = s.hi_b = s.shift = s.c_hi = 0;
-  s.bin_hi = 0;
-  s.c_base = 0;
-  s.nudf = 0;
-#ifdef LSK_PROFILE
-  s.pdead = s.pslots = 0;
-  s.pband = false;
-#endif
-
-  int64_t total_pts = 0;
-  for (int t = 0; t < A.ntrees; t++) total_pts += pick_tree(A, t).n;
-
-  uint32_t hist_passes = 0, limit = 0;
-  if (!valid || total_pts < (int64_t)k) {
-    s.state = ST_DONE;
-    s.hi_b = 0;
-    s.lo_b = cut_b;
-    qs |= QS_DONE_CUT;
+  if (!STRIDE) {
+    const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
+    const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid;
+#include "knn_rows_wave.inc"
   } else {
-    s.state = ST_HIST;
-    const float ub = A.init_d2 ? A.init_d2[qi] : -1.f;
-    if (ub >= 0.f && ub < inf) {
-      // known upper bound (re-query): range ends just above it, no overflow possible
-      const uint32_t top_b = fbits(ub) + 1u;
-      const uint32_t span = (uint32_t)kBins << kShift0;
-      set_range(s, top_b > span ? top_b - span : 0u, kShift0, min(top_b, cut_lim), kUnknown);
-    } else {
-      const uint32_t est_b = fbits(r_est2);
-      const uint32_t off = (uint32_t)(kBins - kTopBins) << kShift0;  // top kTopBins/8 oct. above
-      const uint32_t lo0 = est_b > off ? est_b - off : 0u;
-      if (zero_est) {
-        // zero probe: bins of single float bits from 0 (bin 0 = exact zeros); if fewer
-        // than k values are that small, the overflow resumes at lo0 (band_lo/band_w are
-        // unused while histogramming and carry it)
-        set_range(s, 0u, 0u, cut_lim, kUnknown);
-        s.band_lo = lo0;
-        s.band_w = 1u;
-      } else {
-        set_range(s, lo0, kShift0, cut_lim, kUnknown);
-      }
-    }
-  }
-
-  uint32_t pool_off = 0;
-  bool first = true;
-  uint32_t passes = 0;
-  // terminates: every round runs >= 1 pass (a round that does not break refines at
-  // least one lane: total > kPool implies some lane has bc > kPool / 64), and the
-  // passes are capped at kMaxPasses
-  for (;;) {
-    while (__ballot(s.state == ST_HIST)) {
-      if (++passes > kMaxPasses) {
-        // every unresolved lane (histogramming or waiting for the collect) goes to the
-        // exact backstop
-        limit = 1;
-        if (s.state != ST_DONE) {
-          s.state = ST_DONE;
-          s.lo_b = kNaNBits;
-          qs |= QS_LIMIT | QS_FAIL;
-        }
-        break;
-      }
-      hist_passes++;
-      if (s.state != ST_HIST) {  // not histogramming this pass: count nothing
-        s.hi_b = 0;
-        s.c_hi = 0;
-        s.bin_hi = 0;
-      }
-#pragma unroll 8
-      for (int j = 0; j < kPool / lsk::kWave; j++) W.L->pool[j * lsk::kWave + lane] = 0u;
-      if (kPool % lsk::kWave != 0 && lane < kPool % lsk::kWave)
-        W.L->pool[kPool - kPool % lsk::kWave + lane] = 0u;
-      // pass 1 walks and logs; later passes replay the log when it is complete
-      W.logging = first;
-      if (first) W.log_ok = true;
-      LSK_PT(tt0);
-      if (!first && W.log_ok)
-        traverse<MODE_HIST, true, NT>(s, W, A);
-      else
-        traverse<MODE_HIST, false, NT>(s, W, A);
-      LSK_PADD(W.prof[2], tt0);
-      if (W.crowd) {
-        // aborted pass: counts are partial, but a shrunk top is still a valid bound (at
-        // least k values lie below it). Crowded lanes restart on their crowded bin in
-        // kBins finer bins (a k-th below it comes back through the underflow path), the
-        // others restart on their current range. The log is incomplete from here on.
-        W.crowd = false;
-        W.log_ok = false;
-        W.logging = false;
-        first = false;
-        if (s.state == ST_HIST) {
-          const uint32_t top = top_count(s, W.L->pool, lane);
-          if (s.c_hi >= k && top > (uint32_t)LSK_CROWD_ABORT * k && crowd_refinable(s)) {
-            qs |= QS_REFINE;
-            const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;
-            if (s.bin_hi >= 2) {
-              const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
-              set_range(s, bl, sh, s.hi_b, kUnknown);
-            } else if (s.c_base == kUnknown && s.nudf == 0) {
-              qs |= QS_UNDERFLOW;
-              underflow_restart(s, true);
-            } else {
-              set_range(s, s.lo_b, sh, s.hi_b, s.c_base);
-            }
-          } else {
-            set_range(s, s.lo_b, s.shift, s.hi_b > s.lo_b ? s.hi_b : cut_lim, s.c_base);
-          }
-        }
-        continue;
-      }
-      if (W.logging && W.log_ok) log_prune(W);
-      W.logging = false;
-      first = false;
-      bool ovf = false;
-      if (s.state == ST_HIST && !hist_consistent(s, W.L->pool, lane)) {
-        s.state = ST_DONE;  // a 16-bit bin wrapped: counts are unusable
-        s.lo_b = kNaNBits;
-        qs |= QS_BINOVF | QS_FAIL;
-      }
-      if (s.state == ST_HIST) {
-        const uint32_t top = top_count(s, W.L->pool, lane);
-        if (s.c_hi < k) {
-          if (s.hi_b >= cut_lim) {
-            s.state = ST_DONE;
-            s.lo_b = cut_b;
-            qs |= QS_DONE_CUT;
-          } else {
-            ovf = true;
-            qs |= QS_OVERFLOW;
-            if (s.band_w != 0u && s.band_lo > s.hi_b) {
-              // failed zero probe: back to the estimate's range (count below it unknown)
-              set_range(s, s.band_lo, kShift0, cut_lim, kUnknown);
-            } else {
-              set_range(s, s.hi_b, kShift0, cut_lim, s.c_hi);
-            }
-            s.band_lo = s.band_w = 0u;
-          }
-        } else if (s.bin_hi <= 1 && s.c_base == kUnknown) {
-          // k-th in bin 0, which also holds every value below lo_b: the estimate was
-          // too large. First time: the 8 octaves below. Again: everything below, in 64
-          // coarse bins (then refined) — also how a k-th distance of 0 is reached.
-          qs |= QS_UNDERFLOW;
-          underflow_restart(s, false);
-        } else {
-          // band = bin bin_hi-1; bin 0 loses its saturated part (c_base values < lo_b)
-          const uint32_t below = s.bin_hi == 1 ? s.c_base : s.c_hi - top;
-          const uint32_t bl = s.lo_b + ((uint32_t)(s.bin_hi - 1) << s.shift);
-          const uint32_t bw = s.hi_b - bl;
-          if (bw <= 1u) {
-            s.state = ST_DONE;
-            s.lo_b = bl;
-            qs |= QS_DONE_BAND1;
-          } else {
-            s.state = ST_READY;
-            s.band_lo = bl;
-            s.band_w = bw;
-            s.c_base = below;  // READY: the count below the band (the band's rank is k - below)
-            s.bc = s.c_hi - below;
-          }
-        }
-      }
-      if (__ballot(ovf)) W.log_ok = false;  // the next range lies above pass 1's bound
-    }
-    if (limit) break;
-    const uint32_t need = s.state == ST_READY ? s.bc : 0u;
-    uint32_t x = need;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    const uint32_t total = __shfl(x, 63);
-    pool_off = x - need;
-    if (total <= (uint32_t)kPool) break;
-    if (s.state == ST_READY && s.bc > (uint32_t)(kPool / lsk::kWave)) {
-      qs |= QS_REFINE;
-      const uint32_t sh = s.shift >= kLogBins ? s.shift - kLogBins : 0u;  // kBins bins cover the band
-      set_range(s, s.band_lo, sh, s.band_lo + s.band_w, s.c_base);
-      s.band_lo = s.band_w = 0;
-      s.state = ST_HIST;
-    }
-  }
-
-  if (!W.log_ok) qs |= QS_LIST_INVALID;
-  if (!limit && __ballot(s.state == ST_READY)) {
-    if (s.state != ST_READY) s.band_lo = s.band_w = 0;
-    s.coff = pool_off;
-    s.ccnt = 0;
-    LSK_PT(tc0);
-    if (W.log_ok)
-      traverse<MODE_COLLECT, true, NT>(s, W, A);
-    else
-      traverse<MODE_COLLECT, false, NT>(s, W, A);
-    LSK_PADD(W.prof[3], tc0);
-    LSK_PT(ts0);
-    if (s.state == ST_READY) {
-      qs |= QS_COLLECTED;
-      if (s.ccnt != s.bc) qs |= QS_MISMATCH | QS_FAIL;
-      uint32_t *h = W.L->pool + s.coff;
-      const uint32_t c = min(s.ccnt, s.bc), m = k - s.c_base;
-      if (!(qs & QS_FAIL) && m >= 1 && m <= c) {
-        for (int i = (int)(m / 2) - 1; i >= 0; i--) heap_sift(h, (uint32_t)i, m);
-        for (uint32_t i = m; i < c; i++) {
-          const uint32_t v = h[i];
-          if (v < h[0]) {
-            h[0] = v;
-            heap_sift(h, 0, m);
-          }
-        }
-        s.lo_b = h[0];
-      } else {
-        qs |= QS_MISMATCH | QS_FAIL;
-        s.lo_b = kNaNBits;
-      }
-    }
-    LSK_PADD(W.prof[6], ts0);
-  }
-
-  // a truncated walk (watchdog or step budget: every later pass stops at once, so its
-  // decisions may rest on partial counts) invalidates the whole wave; tests can force
-  // failures
-  if (W.guard) qs |= QS_FAIL;
-  if (A.debug_fail_mod > 0 && qi % A.debug_fail_mod == 0) qs |= QS_FAIL;
-  const bool failed = valid && (qs & QS_FAIL);
-  if (failed) s.lo_b = kNaNBits;
-  if (A.fail_count) {
-    // failure list: one atomic per wave with failures, lanes write their slots
-    const uint64_t fm = __ballot(failed);
-    if (fm) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(A.fail_count, (uint32_t)__popcll(fm));
-      base = lsk::uniform(base);
-      const uint64_t slot = (uint64_t)base + (uint64_t)__popcll(fm & ((1ull << lane) - 1ull));
-      if (failed && slot < (uint64_t)A.fail_cap) A.fail_list[slot] = (uint32_t)qi;
-    }
-  }
-
-  if (valid) {
-    if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(s.lo_b));
-    if (A.out_d2) A.out_d2[qi] = bitsf(s.lo_b);
-#ifdef LSK_PROFILE  // debug: wave cycles (>> 16) in place of the pass count
-    if (A.qstatus)
-      A.qstatus[qi] = qs | ((uint32_t)min((__builtin_readcyclecounter() - twave0) >> 16, (uint64_t)0xffff) << 16);
-#else
-    if (A.qstatus) A.qstatus[qi] = qs | (hist_passes << 16);
-#endif
-  }
-
-#ifdef LSK_PROFILE
-  LSK_PADD(W.prof[7], twave0);
-  if (A.stats && lane == 0)
-    for (int i = 0; i < 8; i++) atomicAdd(&A.stats[16 + i], (unsigned long long)W.prof[i]);
-  if (A.stats && lane == 0) {
-    atomicAdd(&A.stats[24], (unsigned long long)W.prof_rows_entry);
-    atomicAdd(&A.stats[25], (unsigned long long)W.prof_rows_in);
-    atomicAdd(&A.stats[28], (unsigned long long)s.pdead);
-    atomicAdd(&A.stats[29], (unsigned long long)s.pslots);
-    atomicAdd(&A.stats[30], (unsigned long long)W.prof_crows_entry);
-    atomicAdd(&A.stats[31], (unsigned long long)W.prof_crows_in);
-  }
-#endif
-  if (A.stats) {
-    auto cnt = [&](uint32_t bit) {
-      return (unsigned long long)__popcll(__ballot(valid && (qs & bit)));
-    };
-    const unsigned long long c_ovf = cnt(QS_OVERFLOW), c_udf = cnt(QS_UNDERFLOW),
-                             c_ref = cnt(QS_REFINE), c_mm = cnt(QS_MISMATCH), c_hint = cnt(QS_HINT),
-                             c_fail = cnt(QS_FAIL), c_bovf = cnt(QS_BINOVF);
-    if (lane == 0) {
-      atomicAdd(&A.stats[0], (unsigned long long)W.steps * 16ull);  // candidates per lane
-      atomicAdd(&A.stats[1], (unsigned long long)W.quarters);
-      atomicAdd(&A.stats[2], (unsigned long long)W.nodes_visited);
-      atomicAdd(&A.stats[3], (unsigned long long)hist_passes);
-      atomicAdd(&A.stats[4], c_ovf);
-      atomicAdd(&A.stats[5], c_udf);
-      atomicAdd(&A.stats[6], c_ref);
-      atomicAdd(&A.stats[7], c_mm);
-      atomicAdd(&A.stats[8], (unsigned long long)limit);
-      atomicAdd(&A.stats[9], W.log_ok ? 0ull : 1ull);
-      atomicAdd(&A.stats[10], 1ull);
-      atomicAdd(&A.stats[11], c_hint);
-      atomicAdd(&A.stats[12], (unsigned long long)W.steps);
-      atomicAdd(&A.stats[13], (unsigned long long)W.csteps);
-      atomicAdd(&A.stats[14], (unsigned long long)W.cnodes);
-      atomicAdd(&A.stats[15], (unsigned long long)W.guard);
-      atomicAdd(&A.stats[26], c_fail);
-      atomicAdd(&A.stats[27], c_bovf);
+    if (A.gate && *A.gate != A.gate_on) return;
+    const uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+    for (uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid; w < nwaves;
+         w += (uint64_t)gridDim.x * kWavesPerBlock) {
+      [&](const uint64_t wave) {
+#include "knn_rows_wave.inc"
+      }(w);
     }
   }
 }
@@ -1445,6 +1070,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 #ifndef LSK_RCAP
 #define LSK_RCAP 32  // row queue capacity (entries per row, a power of two <= 32)
 #endif
+constexpr unsigned kStrideBlocks = 1024;  // persistent form: 2048 waves, 2 per SIMD
 
 extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const lsk_knn_args &A = *args;
@@ -1468,10 +1094,18 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   // Row work-queue capacity 32 entries per row: 5.6 KB of LDS per wave, 28 waves
   // per CU. One instance per tree count: the single-tree one (every local pass) has no
   // per-lane tree selects in its step loop; the two-tree one serves halo re-queries.
-  if (A.ntrees > 1)
-    knn_rows_kernel<LSK_RCAP, 2><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
-  else
-    knn_rows_kernel<LSK_RCAP, 1><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A);
+  hipStream_t st = (hipStream_t)stream;
+  if (A.pad2 == 1) {  // persistent strided form (see knn_rows_kernel)
+    const unsigned sblk = nblk < kStrideBlocks ? nblk : kStrideBlocks;
+    if (A.ntrees > 1)
+      knn_rows_kernel<LSK_RCAP, 2, true><<<sblk, kThreads, 0, st>>>(A);
+    else
+      knn_rows_kernel<LSK_RCAP, 1, true><<<sblk, kThreads, 0, st>>>(A);
+  } else if (A.ntrees > 1) {
+    knn_rows_kernel<LSK_RCAP, 2, false><<<nblk, kThreads, 0, st>>>(A);
+  } else {
+    knn_rows_kernel<LSK_RCAP, 1, false><<<nblk, kThreads, 0, st>>>(A);
+  }
   LSK_CHECK_LAUNCH("knn_rows");
   return 0;
 }

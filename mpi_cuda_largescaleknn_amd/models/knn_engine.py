@@ -67,6 +67,9 @@ GRID = os.environ.get("LSKNN_GRID", "auto")
 GRID_MS = float(os.environ.get("LSKNN_GRID_MS", "6"))  # target mean points per finest cell
 # auto: a point's sub-cell holds on average at most this many times the mean (+1)
 GRID_CROWD = float(os.environ.get("LSKNN_GRID_CROWD", "2"))
+# Which kernel the device gate is expected to pick (the last decision read on the host):
+# that one gets the full launch, the other a small persistent one (kernels.knn_gpu).
+GRID_EXPECT = [True]
 
 
 @dataclass
@@ -481,12 +484,16 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
             KERNELS_USED.add("grid" if use_grid else impl)
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
-                   grid=index.grid.view() if use_grid else None, ngroups_dev=ngroups_dev, **kw)
+                   grid=index.grid.view() if use_grid else None, ngroups_dev=ngroups_dev,
+                   expect_grid=GRID_EXPECT[0], **kw)
+    gate = index.grid.gate if use_grid else None
     def check() -> bool:
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun
         # the whole query on the exact kernel (on the current stream; returns True then)
         nfail = fw.value()
         rerun = nfail > fw.cap
+        if gate is not None:  # (the launch is complete: reading its decision costs nothing)
+            GRID_EXPECT[0] = bool(int(gate.item()))
         if rerun:
             K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", ngroups_dev=ngroups_dev,
                       **kw)

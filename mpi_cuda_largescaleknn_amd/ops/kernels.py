@@ -319,7 +319,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             stats: torch.Tensor | None = None, qstatus: torch.Tensor | None = None,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
-            debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None) -> FailWord:
+            debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None,
+            expect_grid: bool = True) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -335,6 +336,9 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     debug_fail_mod (tests): the rows kernel also fails every query q with q % mod == 0.
     ngroups_dev (optional, with groups): int32 [1] on the device, the list's length
     (ngroups is then only the launch's upper bound).
+    expect_grid (with a gate): which kernel the gate is expected to pick — that one gets the
+    full launch, the other its persistent strided form (a small grid whose waves return at
+    once when the gate rejects it; a misprediction costs speed, never exactness).
     grid (impl "grid"): (slots, level, box, inf4[, gate]) of knn_engine.GridIndex — the
     cell-grid candidate source of knn_grid.hip for one tree whose points are the queries
     (same failure list and backstop as "rows"); with a device gate (int32 [1]) the grid
@@ -397,11 +401,14 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             # not chosen returns at its first instruction (no host read, graph-capturable)
             a.gate = _ptr(gate)
             a.gate_on = 1
+            a.pad2 = 0 if expect_grid else 1
         check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
         if gate is not None:
             a.gate_on = 0
+            a.pad2 = 1 if expect_grid else 0
             check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
         a.gate = None
+        a.pad2 = 0
     else:
         check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
     # exact backstop over the failure list (device-side count: empty list = short no-op)

@@ -195,3 +195,20 @@ def test_grid_knn_large_k_counter_wraps():
     for k in (2000, 6000):
         got, _, st = grid_knn(p, k)
         assert torch.equal(got, oracle(p, k)), (k, st.counters)
+
+
+@pytest.mark.parametrize("expect", [True, False])
+def test_gate_misprediction_runs_the_persistent_form(expect, monkeypatch):
+    """The kernel the gate is not expected to pick gets a small persistent (strided)
+    launch: a wrong expectation still gives exact results — uniform data with the rows
+    kernel expected (the grid kernel strides), mixed-scale data with the grid expected
+    (the rows kernel strides)."""
+    monkeypatch.setattr(E, "GRID", "auto")
+    for gen in ("uniform", "mixed_scale"):
+        p = GENERATORS[gen](120_000, seed=4)
+        monkeypatch.setattr(E, "GRID_EXPECT", [expect])
+        idx = E.build_index(p.to(DEV), grid=True)
+        out = torch.empty(idx.n, dtype=torch.float32, device=DEV)
+        E.query(idx, E.KnnConfig(k=32), E.radius_hint(idx.box, idx.n, 32), final_out=out)
+        assert torch.equal(out.cpu(), oracle(p, 32)), gen
+        assert E.GRID_EXPECT[0] == (gen == "uniform")  # updated from the decision
