@@ -19,8 +19,10 @@
 //     trees (DFS, 8-ary expansion tested by 8 lanes, stack in LDS), prunes boxes whose
 //     distance is >= hi and boxes whose farthest corner is closer than lo (their values
 //     were counted by an earlier pass: a thin shell through a dense far cluster visits
-//     only the buckets it cuts), and counts the values of each 64-point bucket (one point per
-//     lane) into 256 32-bit LDS bins. The bin holding the k-th value becomes the next
+//     only the buckets it cuts), counts a whole box at once when its [near, far] range
+//     falls in one bin (subtree point count from the implicit tree), and counts the values
+//     of each remaining 64-point bucket (one point per lane, one wave-wide atomic when
+//     they share a bin) into 256 32-bit LDS bins. The bin holding the k-th value becomes the next
 //     [lo, hi); a range of width 1 is the answer. <= 4 counting passes (8 bits each).
 // Same canonical dist² (common.h) as the oracle and the production kernel: bit-identical.
 #include "dev.h"
@@ -61,9 +63,19 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
     if (lvl >= depth) {  // a bucket: one point per lane
       const int64_t b = (int64_t)node - ((int64_t)1 << depth);
       const int64_t i = b * lsk::kBucket + lane;
-      if (i < T.n) {
-        const uint32_t v = cand_bits(qx, qy, qz, T.pts + 3 * i);
-        if (v >= lo && v < hi) atomicAdd(&L.hist[(v - lo) >> shift], 1u);
+      const uint32_t v = i < T.n ? cand_bits(qx, qy, qz, T.pts + 3 * i) : hi;
+      const bool in = v >= lo && v < hi;
+      const uint32_t bin = (v - lo) >> shift;
+      // a far query sees a dense bucket's values in one or a few bins: one atomic for
+      // the wave when they all share a bin (same-address LDS atomics serialise)
+      const uint64_t m = __ballot(in);
+      if (m) {
+        const uint32_t b0 = lsk::uniform((uint32_t)__shfl((int)bin, (int)__builtin_ctzll(m)));
+        if (__ballot(in && bin == b0) == m) {
+          if (lane == 0) atomicAdd(&L.hist[b0], (uint32_t)__popcll(m));
+        } else if (in) {
+          atomicAdd(&L.hist[bin], 1u);
+        }
       }
       continue;
     }
@@ -75,15 +87,28 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
     bool need = false;
     if ((uint32_t)lane < nc) {
       const float4 lo4 = nodes[2 * child], hi4 = nodes[2 * child + 1];
-      need = lsk::box_dist2(q, {lo4.x, lo4.y, lo4.z}, {hi4.x, hi4.y, hi4.z}) < lim;
-      if (need && lo > 0u) {
-        // shell test: a box whose farthest corner is closer than bitsf(lo) holds only
-        // values below lo, already counted by the previous passes (per-axis float
-        // differences, squares and fma are monotone: no point inside is farther)
+      const float nd = lsk::box_dist2(q, {lo4.x, lo4.y, lo4.z}, {hi4.x, hi4.y, hi4.z});
+      need = nd < lim;
+      if (need) {
+        // farthest corner (per-axis float differences, squares and fma are monotone: no
+        // point inside is farther)
         const float fx = fmaxf(fabsf(lo4.x - qx), fabsf(hi4.x - qx));
         const float fy = fmaxf(fabsf(lo4.y - qy), fabsf(hi4.y - qy));
         const float fz = fmaxf(fabsf(lo4.z - qz), fabsf(hi4.z - qz));
-        need = fbits(lsk::dist2(fx, fy, fz)) >= lo;
+        const uint32_t fb = fbits(lsk::dist2(fx, fy, fz)), nb = fbits(nd);
+        if (fb < lo) {
+          // shell test: only values below lo, counted by the previous passes
+          need = false;
+        } else if (nb >= lo && fb < hi && ((nb - lo) >> shift) == ((fb - lo) >> shift)) {
+          // the whole subtree falls in one bin: count it without visiting its points
+          // (a far query looking at a dense cluster resolves the coarse passes per box)
+          const int32_t span_lg = depth - (lvl + step);
+          const int64_t first = ((int64_t)child - ((int64_t)1 << (lvl + step))) << span_lg;
+          const int64_t p0 = first * lsk::kBucket;
+          const int64_t p1 = min(T.n, (first + ((int64_t)1 << span_lg)) * lsk::kBucket);
+          if (p1 > p0) atomicAdd(&L.hist[(nb - lo) >> shift], (uint32_t)(p1 - p0));
+          need = false;
+        }
       }
     }
     const uint64_t m = __ballot(need);

@@ -611,6 +611,8 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
 // one scan of all points when the tree is small, else the wave hands its unresolved
 // queries to the exact backstop (returns false).
 constexpr unsigned kStrideBlocks = 1024;  // persistent form: 2048 waves, 2 per SIMD
+constexpr unsigned kStrideBlocksFull = 4096;  // persistent form over a short group list: 8192
+                                              // waves, the kernel's full occupancy
 constexpr uint32_t kMaxCells = 4096;
 // Candidate budget of a wave, checked before each pass: max(kEvalBudget, kEvalsPerK * k),
 // ~80x a uniform wave at k = 100 (~3.4K). Beyond it the wave's unresolved queries go to
@@ -732,7 +734,9 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
 // STRIDE = false: one wave per group (the normal launch). STRIDE = true: a small persistent
 // grid strides over the groups — the form launched when the device gate is expected to
 // pick knn_rows: every wave returns at once when it does, instead of millions of blocks
-// each being dispatched only to return (1B points: ~16 ms per launch).
+// each being dispatched only to return (1B points: ~16 ms per launch); and, at full
+// occupancy, over a group list whose device-side length is far below its bound (a rank's
+// boundary groups: ~5 % of its groups).
 template <bool STRIDE>
 __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
   __shared__ uint32_t lds[kWPB][kPool + 8 * kCullGroups];
@@ -744,7 +748,8 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
 #include "knn_grid_wave.inc"
   } else {
     if (A.gate && *A.gate != A.gate_on) return;
-    const uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+    uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+    if (A.groups && A.ngroups_dev) nwaves = min(nwaves, (uint64_t)*A.ngroups_dev);
     for (uint64_t w = (uint64_t)blockIdx.x * kWPB + wid; w < nwaves; w += (uint64_t)gridDim.x * kWPB) {
       [&](const uint64_t wave) {
 #include "knn_grid_wave.inc"
@@ -934,8 +939,10 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
   if (ngroups <= 0) return 0;
   const unsigned nblk = lsk_blocks(ngroups, kWPB);
-  if (A.pad2 == 1)  // persistent strided form (see knn_grid_kernel)
-    knn_grid_kernel<true><<<nblk < kStrideBlocks ? nblk : kStrideBlocks, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+  if (A.pad2 >= 1) {  // persistent strided form (see knn_grid_kernel); 2: a short list
+    const unsigned cap = A.pad2 == 2 ? kStrideBlocksFull : kStrideBlocks;
+    knn_grid_kernel<true><<<nblk < cap ? nblk : cap, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+  }
   else
     knn_grid_kernel<false><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
   LSK_CHECK_LAUNCH("knn_grid");

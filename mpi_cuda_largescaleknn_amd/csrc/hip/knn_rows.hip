@@ -1055,7 +1055,8 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 #include "knn_rows_wave.inc"
   } else {
     if (A.gate && *A.gate != A.gate_on) return;
-    const uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+    uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
+    if (A.groups && A.ngroups_dev) nwaves = min(nwaves, (uint64_t)*A.ngroups_dev);
     for (uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid; w < nwaves;
          w += (uint64_t)gridDim.x * kWavesPerBlock) {
       [&](const uint64_t wave) {
@@ -1071,6 +1072,7 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
 #define LSK_RCAP 32  // row queue capacity (entries per row, a power of two <= 32)
 #endif
 constexpr unsigned kStrideBlocks = 1024;  // persistent form: 2048 waves, 2 per SIMD
+constexpr unsigned kStrideBlocksFull = 4096;  // ... over a short group list (pad2 = 2)
 
 extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   const lsk_knn_args &A = *args;
@@ -1095,8 +1097,9 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
   // per CU. One instance per tree count: the single-tree one (every local pass) has no
   // per-lane tree selects in its step loop; the two-tree one serves halo re-queries.
   hipStream_t st = (hipStream_t)stream;
-  if (A.pad2 == 1) {  // persistent strided form (see knn_rows_kernel)
-    const unsigned sblk = nblk < kStrideBlocks ? nblk : kStrideBlocks;
+  if (A.pad2 >= 1) {  // persistent strided form (see knn_rows_kernel); 2: a short list
+    const unsigned cap = A.pad2 == 2 ? kStrideBlocksFull : kStrideBlocks;
+    const unsigned sblk = nblk < cap ? nblk : cap;
     if (A.ntrees > 1)
       knn_rows_kernel<LSK_RCAP, 2, true><<<sblk, kThreads, 0, st>>>(A);
     else

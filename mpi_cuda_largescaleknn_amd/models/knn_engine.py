@@ -426,7 +426,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
           init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None,
           keep_d2: bool = False, deferred: list | None = None,
-          ngroups_dev: torch.Tensor | None = None) -> torch.Tensor:
+          ngroups_dev: torch.Tensor | None = None, short_list: bool = False) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
     `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order.
 
@@ -438,7 +438,8 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     on the list; `settle(deferred)` does it later — the launch stays asynchronous, so the
     host can queue other work (the overlapped halo exchange) behind it.
     `ngroups_dev` (with `groups`): the list's length as an int32 [1] tensor (on the GPU it
-    stays on the device; `ngroups` is then the launch's upper bound)."""
+    stays on the device; `ngroups` is then the launch's upper bound); `short_list`: that
+    length is expected far below ngroups (kernels.knn_gpu)."""
     n = index.n
     want_d2 = final_out is None or keep_d2 or out is not None
     if out is None and want_d2:
@@ -485,15 +486,15 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
                    grid=index.grid.view() if use_grid else None, ngroups_dev=ngroups_dev,
-                   expect_grid=GRID_EXPECT[0], **kw)
+                   expect_grid=GRID_EXPECT[0], short_list=short_list, **kw)
     gate = index.grid.gate if use_grid else None
     def check() -> bool:
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun
         # the whole query on the exact kernel (on the current stream; returns True then)
         nfail = fw.value()
         rerun = nfail > fw.cap
-        if gate is not None:  # (the launch is complete: reading its decision costs nothing)
-            GRID_EXPECT[0] = bool(int(gate.item()))
+        if gate is not None:  # (staged with the failure word: no wait for later work)
+            GRID_EXPECT[0] = bool(fw.gate_value(gate))
         if rerun:
             K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, impl="exact", ngroups_dev=ngroups_dev,
                       **kw)
@@ -514,7 +515,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
         if stats is not None:
             stats.add(raw)
     elif deferred is not None:
-        fw.stage()  # the later read waits for this launch only
+        fw.stage(gate)  # the later read waits for this launch only
         deferred.append(check)
     else:
         check()

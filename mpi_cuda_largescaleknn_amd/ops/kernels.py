@@ -288,17 +288,29 @@ class FailWord:
         self.cap = cap
         self._host = None
         self._ev = None
+        self._gate = None
 
-    def stage(self) -> None:
+    def stage(self, gate: torch.Tensor | None = None) -> None:
         """Queue the word's copy to pinned host memory on the current stream (right behind
         the launch): a later value() waits for this launch only, not for work queued on
-        the stream after it."""
+        the stream after it. `gate` (the device grid decision, int32 [1]) is staged with it
+        (gate_value()): a .item() would wait for everything queued on the stream since."""
         if self.count is None or self.count.device.type != "cuda":
             return
-        self._host = torch.empty(1, dtype=self.count.dtype, pin_memory=True)
-        self._host.copy_(self.count, non_blocking=True)
+        self._host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        self._host[0:1].copy_(self.count.view(torch.int32), non_blocking=True)
+        if gate is not None:
+            self._host[1:2].copy_(gate.view(-1)[:1].to(torch.int32), non_blocking=True)
+            self._gate = gate
         self._ev = torch.cuda.Event()
         self._ev.record()
+
+    def gate_value(self, gate: torch.Tensor) -> int:
+        """The staged grid decision (stage(gate)), else a direct read."""
+        if self._gate is gate and self._ev is not None:
+            self._ev.synchronize()
+            return int(self._host[1])
+        return int(gate.item())
 
     def value(self) -> int:
         # the kernels count in uint32 (a count >= 2^31 must not read as negative)
@@ -320,7 +332,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
             debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None,
-            expect_grid: bool = True) -> FailWord:
+            expect_grid: bool = True, short_list: bool = False) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -339,6 +351,10 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     expect_grid (with a gate): which kernel the gate is expected to pick — that one gets the
     full launch, the other its persistent strided form (a small grid whose waves return at
     once when the gate rejects it; a misprediction costs speed, never exactness).
+    short_list (with ngroups_dev): the device-side list is expected far shorter than
+    ngroups (a rank's boundary groups): the kernel that runs takes its persistent strided
+    form at full occupancy instead of one wave per possible group (most would be
+    dispatched only to return: ~16 ms per 1M-block launch).
     grid (impl "grid"): (slots, level, box, inf4[, gate]) of knn_engine.GridIndex — the
     cell-grid candidate source of knn_grid.hip for one tree whose points are the queries
     (same failure list and backstop as "rows"); with a device gate (int32 [1]) the grid
@@ -392,6 +408,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_list = _ptr(flist)
     a.fail_count = _ptr(count)
     a.fail_cap = cap
+    full = 2 if short_list and groups is not None and ngroups_dev is not None else 0
     if impl == "grid":
         slots, level, gbox, inf4 = grid[:4]
         gate = grid[4] if len(grid) > 4 else None
@@ -401,16 +418,20 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             # not chosen returns at its first instruction (no host read, graph-capturable)
             a.gate = _ptr(gate)
             a.gate_on = 1
-            a.pad2 = 0 if expect_grid else 1
+            a.pad2 = full if expect_grid else 1
+        else:
+            a.pad2 = full
         check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
         if gate is not None:
             a.gate_on = 0
-            a.pad2 = 1 if expect_grid else 0
+            a.pad2 = 1 if expect_grid else full
             check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
         a.gate = None
         a.pad2 = 0
     else:
+        a.pad2 = full
         check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
+        a.pad2 = 0
     # exact backstop over the failure list (device-side count: empty list = short no-op)
     check(lib.lsk_hip_knn_exact(C.byref(a), _ptr(flist), _ptr(count), cap, st), "knn_exact")
     return FailWord(count, cap)

@@ -587,7 +587,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         # 2. the boundary groups' local pass first: their exact radii (interior leaves 0)
         #    are what the other ranks filter their points with
         E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=blist, ngroups=ng,
-                ngroups_dev=bcnt, deferred=pend if gpu else None)
+                ngroups_dev=bcnt, deferred=pend if gpu else None, short_list=True)
         radii = K.tree_set_radii(index.nodes.clone(), n, d2)
         if gpu:
             ev_rad = torch.cuda.Event()

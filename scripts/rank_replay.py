@@ -111,7 +111,8 @@ for r in range(P):
     fin = torch.empty(nr, dtype=torch.float32, device=DEV)
 
     def local():
-        E.query(index, cfg, hint2, out=d2, final_out=fin, groups=blist, ngroups=ng, ngroups_dev=bcnt)
+        E.query(index, cfg, hint2, out=d2, final_out=fin, groups=blist, ngroups=ng, ngroups_dev=bcnt,
+                short_list=True)
         E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng, ngroups_dev=icnt)
 
     _, t_local = timed(local)

@@ -212,3 +212,32 @@ def test_gate_misprediction_runs_the_persistent_form(expect, monkeypatch):
         E.query(idx, E.KnnConfig(k=32), E.radius_hint(idx.box, idx.n, 32), final_out=out)
         assert torch.equal(out.cpu(), oracle(p, 32)), gen
         assert E.GRID_EXPECT[0] == (gen == "uniform")  # updated from the decision
+
+
+@pytest.mark.parametrize("gen", ["uniform", "mixed_scale"])
+def test_short_group_list_strided_launch(gen, monkeypatch):
+    """A device-counted group list far shorter than its bound (a rank's boundary groups)
+    runs in the persistent strided form at full occupancy (short_list): the listed groups
+    get exactly the whole-set result, the others stay untouched — grid (uniform) and rows
+    (mixed-scale: the gate picks knn_rows) kernels, with the count below the bound."""
+    monkeypatch.setattr(E, "GRID", "auto")
+    p = GENERATORS[gen](200_000, seed=6)
+    idx = E.build_index(p.to(DEV), grid=True)
+    cfg = E.KnnConfig(k=100)
+    hint2 = E.radius_hint(idx.box, idx.n, 100)
+    full = E.query(idx, cfg, hint2)
+    ng = (idx.n + 63) // 64
+    g = torch.Generator().manual_seed(1)
+    sel = torch.randperm(ng, generator=g)[:ng // 20].sort().values.to(torch.int32)
+    lst = torch.full((ng,), -1, dtype=torch.int32)
+    lst[:sel.numel()] = sel
+    cnt = torch.tensor([sel.numel()], dtype=torch.int32)
+    d2 = torch.full((idx.n,), -7.0, device=DEV)
+    E.query(idx, cfg, hint2, out=d2, groups=lst.to(DEV), ngroups=ng, ngroups_dev=cnt.to(DEV),
+            short_list=True)
+    rows = (sel.long()[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
+    rows = rows[rows < idx.n]
+    assert torch.equal(d2.cpu()[rows], full.cpu()[rows])
+    mask = torch.ones(idx.n, dtype=torch.bool)
+    mask[rows] = False
+    assert bool((d2.cpu()[mask] == -7.0).all())
