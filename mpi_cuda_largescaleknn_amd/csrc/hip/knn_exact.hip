@@ -10,7 +10,8 @@
 // This is the exactness guarantee of the reference's FlexHeapCandidateList +
 // stackFree::knn (unorderedDataVariant.cu:84-86, 97-102), without its N*k heap memory.
 //
-// Per query (one wave, all control flow wave-uniform):
+// Per query (one wave, all control flow wave-uniform; a failure list gives each query a
+// block of 8 waves that split every tree's buckets and share the histogram):
 //  1. Upper bound: the max d² over k points taken around the query's position in
 //     tree 0 (queries are tree points in curve order, so these are spatial neighbours;
 //     any k distinct points give a valid bound), tightened by init_d2 when given, and
@@ -32,33 +33,49 @@ namespace {
 using lsk::bitsf;
 using lsk::fbits;
 
-constexpr int kWaves = 4;  // waves per block
+constexpr int kWaves = 4;      // waves per block, one query each (whole-set runs)
+constexpr int kListWaves = 8;  // waves per block, all on one query (failure lists)
 constexpr int kBins = 256;
 constexpr int kStack = 128;  // DFS stack entries per wave (8-ary: <= 9 * 7 + 1 used)
 
+// W = 1: each wave owns its query (hist per wave). W > 1: the block's W waves share one
+// query and one histogram, each walking a contiguous 1/W of every tree's buckets: the
+// hard failures (a far query resolving a dense cluster point by point) are latency-bound
+// walks, W waves in flight on them instead of one.
+template <int W>
 struct ExactLds {
   uint32_t hist[kBins];
-  uint32_t stk[kStack];
+  uint32_t stk[W][kStack];
 };
+
+template <int W>
+__device__ __forceinline__ void qbarrier() {
+  if constexpr (W == 1)
+    __builtin_amdgcn_wave_barrier();
+  else
+    __syncthreads();
+}
 
 __device__ __forceinline__ uint32_t cand_bits(float qx, float qy, float qz, const float *p) {
   return fbits(lsk::dist2(qx - p[0], qy - p[1], qz - p[2]));
 }
 
-// Histogram every value v in [lo, hi) of the points of one tree into hist[(v-lo)>>shift].
+// Histogram every value v in [lo, hi) of the points of buckets [b0, b1) of one tree into
+// hist[(v-lo)>>shift].
 __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz, uint32_t lo,
-                           uint32_t hi, uint32_t shift, ExactLds &L, int lane) {
-  if (T.n <= 0) return;
+                           uint32_t hi, uint32_t shift, uint32_t *hist, uint32_t *stk, int64_t b0,
+                           int64_t b1, int lane) {
+  if (T.n <= 0 || b0 >= b1) return;
   const int32_t depth = T.depth;
   const float lim = bitsf(hi);  // a box at distance >= bitsf(hi) holds no value < hi
   const lsk::vec3f q{qx, qy, qz};
   const float4 *nodes = (const float4 *)T.nodes;
   uint32_t sp = 1;
-  if (lane == 0) L.stk[0] = 1u;
+  if (lane == 0) stk[0] = 1u;
   __builtin_amdgcn_wave_barrier();
   while (sp > 0) {
     sp--;
-    const uint32_t node = lsk::uniform(L.stk[sp]);
+    const uint32_t node = lsk::uniform(stk[sp]);
     const int32_t lvl = 31 - __clz(node);
     if (lvl >= depth) {  // a bucket: one point per lane
       const int64_t b = (int64_t)node - ((int64_t)1 << depth);
@@ -70,11 +87,11 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
       // the wave when they all share a bin (same-address LDS atomics serialise)
       const uint64_t m = __ballot(in);
       if (m) {
-        const uint32_t b0 = lsk::uniform((uint32_t)__shfl((int)bin, (int)__builtin_ctzll(m)));
-        if (__ballot(in && bin == b0) == m) {
-          if (lane == 0) atomicAdd(&L.hist[b0], (uint32_t)__popcll(m));
+        const uint32_t bf = lsk::uniform((uint32_t)__shfl((int)bin, (int)__builtin_ctzll(m)));
+        if (__ballot(in && bin == bf) == m) {
+          if (lane == 0) atomicAdd(&hist[bf], (uint32_t)__popcll(m));
         } else if (in) {
-          atomicAdd(&L.hist[bin], 1u);
+          atomicAdd(&hist[bin], 1u);
         }
       }
       continue;
@@ -86,9 +103,13 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
     const uint32_t child = (node << step) + (uint32_t)lane;
     bool need = false;
     if ((uint32_t)lane < nc) {
+      // the child's buckets, clipped to this wave's share
+      const int32_t span_lg = depth - (lvl + step);
+      const int64_t first = ((int64_t)child - ((int64_t)1 << (lvl + step))) << span_lg;
+      const int64_t c0 = max(first, b0), c1 = min(first + ((int64_t)1 << span_lg), b1);
       const float4 lo4 = nodes[2 * child], hi4 = nodes[2 * child + 1];
       const float nd = lsk::box_dist2(q, {lo4.x, lo4.y, lo4.z}, {hi4.x, hi4.y, hi4.z});
-      need = nd < lim;
+      need = c0 < c1 && nd < lim;
       if (need) {
         // farthest corner (per-axis float differences, squares and fma are monotone: no
         // point inside is farther)
@@ -100,13 +121,10 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
           // shell test: only values below lo, counted by the previous passes
           need = false;
         } else if (nb >= lo && fb < hi && ((nb - lo) >> shift) == ((fb - lo) >> shift)) {
-          // the whole subtree falls in one bin: count it without visiting its points
-          // (a far query looking at a dense cluster resolves the coarse passes per box)
-          const int32_t span_lg = depth - (lvl + step);
-          const int64_t first = ((int64_t)child - ((int64_t)1 << (lvl + step))) << span_lg;
-          const int64_t p0 = first * lsk::kBucket;
-          const int64_t p1 = min(T.n, (first + ((int64_t)1 << span_lg)) * lsk::kBucket);
-          if (p1 > p0) atomicAdd(&L.hist[(nb - lo) >> shift], (uint32_t)(p1 - p0));
+          // the whole (clipped) subtree falls in one bin: count it without visiting its
+          // points (a far query looking at a dense cluster resolves coarse passes per box)
+          const int64_t p0 = c0 * lsk::kBucket, p1 = min(T.n, c1 * lsk::kBucket);
+          if (p1 > p0) atomicAdd(&hist[(nb - lo) >> shift], (uint32_t)(p1 - p0));
           need = false;
         }
       }
@@ -114,7 +132,7 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
     const uint64_t m = __ballot(need);
     if (need) {
       const uint32_t r = __popcll(m & ((1ull << lane) - 1ull));
-      L.stk[sp + r] = child;
+      stk[sp + r] = child;
     }
     sp += (uint32_t)__popcll(m);
     __builtin_amdgcn_wave_barrier();
@@ -140,7 +158,9 @@ __device__ uint32_t window_bound(const lsk_knn_args &A, int64_t pos, float qx, f
   return lsk::uniform(vmax);
 }
 
-__device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds &L, int lane) {
+// The k-th value of query qi; every wave of the query's group (W) returns it.
+template <int W>
+__device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds<W> &L, int wq, int lane) {
   const uint32_t k = (uint32_t)A.k;
   const float qx = lsk::uniform_f(A.qpts[3 * qi]);
   const float qy = lsk::uniform_f(A.qpts[3 * qi + 1]);
@@ -173,11 +193,15 @@ __device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds &L, in
     if (width == 0u) return cut_b;  // (not reached: hi > lo always holds)
     uint32_t shift = 0;
     while (((width - 1u) >> shift) >= (uint32_t)kBins) shift++;
-#pragma unroll
-    for (int j = 0; j < kBins / lsk::kWave; j++) L.hist[j * lsk::kWave + lane] = 0u;
-    __builtin_amdgcn_wave_barrier();
-    for (int t = 0; t < A.ntrees; t++) count_tree(A.tree[t], qx, qy, qz, lo, hi, shift, L, lane);
-    __builtin_amdgcn_wave_barrier();
+    qbarrier<W>();  // (the previous pass's reads of hist are done)
+    for (int j = wq * lsk::kWave + lane; j < kBins; j += W * lsk::kWave) L.hist[j] = 0u;
+    qbarrier<W>();
+    for (int t = 0; t < A.ntrees; t++) {
+      const int64_t nb = (A.tree[t].n + lsk::kBucket - 1) / lsk::kBucket;
+      count_tree(A.tree[t], qx, qy, qz, lo, hi, shift, L.hist, L.stk[wq], nb * wq / W, nb * (wq + 1) / W,
+                 lane);
+    }
+    qbarrier<W>();
     // lane l owns bins 4l .. 4l+3
     const uint32_t c0 = L.hist[4 * lane], c1 = L.hist[4 * lane + 1];
     const uint32_t c2 = L.hist[4 * lane + 2], c3 = L.hist[4 * lane + 3];
@@ -218,41 +242,46 @@ __device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds &L, in
   return 0x7fc00000u;  // unreachable: width shrinks 256x per pass
 }
 
-__global__ __launch_bounds__(kWaves * 64) void knn_exact_kernel(const lsk_knn_args A,
-                                                                const uint32_t *__restrict__ list,
-                                                                const uint32_t *__restrict__ count,
-                                                                int64_t cap) {
-  __shared__ ExactLds lds[kWaves];
+__device__ __forceinline__ void write_answer(const lsk_knn_args &A, int64_t qi, uint32_t ans) {
+  if (A.out_d2) A.out_d2[qi] = bitsf(ans);
+  if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(ans));
+}
+
+// Whole-set runs (no list): one query per wave, grid-stride over the queries / groups.
+__global__ __launch_bounds__(kWaves * 64) void knn_exact_kernel(const lsk_knn_args A) {
+  __shared__ ExactLds<1> lds[kWaves];
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
-  ExactLds &L = lds[wid];
+  ExactLds<1> &L = lds[wid];
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wid;
   const int64_t tw = (int64_t)gridDim.x * kWaves;
-  int64_t total;
-  if (list) {
-    const int64_t c = (int64_t)count[0];
-    total = c < cap ? c : cap;
-  } else {
-    int64_t ng = A.ngroups;
-    if (A.groups && A.ngroups_dev) ng = min(ng, (int64_t)A.ngroups_dev[0]);
-    total = A.groups ? ng * lsk::kBucket : A.nq;
-  }
+  int64_t ng = A.ngroups;
+  if (A.groups && A.ngroups_dev) ng = min(ng, (int64_t)A.ngroups_dev[0]);
+  const int64_t total = A.groups ? ng * lsk::kBucket : A.nq;
   for (int64_t i = gw; i < total; i += tw) {
-    int64_t qi;
-    if (list) {
-      qi = (int64_t)list[i];
-    } else if (A.groups) {
-      qi = (int64_t)A.groups[i / lsk::kBucket] * lsk::kBucket + (i % lsk::kBucket);
-    } else {
-      qi = i;
-    }
+    int64_t qi = A.groups ? (int64_t)A.groups[i / lsk::kBucket] * lsk::kBucket + (i % lsk::kBucket) : i;
     qi = (int64_t)lsk::uniform((uint32_t)qi);
     if (qi >= A.nq) continue;
-    const uint32_t ans = exact_kth(A, qi, L, lane);
-    if (lane == 0) {
-      if (A.out_d2) A.out_d2[qi] = bitsf(ans);
-      if (A.out_perm) A.out_final[A.out_perm[qi]] = lsk::final_distance(bitsf(ans));
-    }
+    const uint32_t ans = exact_kth<1>(A, qi, L, 0, lane);
+    if (lane == 0) write_answer(A, qi, ans);
+  }
+}
+
+// Failure lists: the block's kListWaves waves on one listed query at a time.
+__global__ __launch_bounds__(kListWaves * 64) void knn_exact_list_kernel(const lsk_knn_args A,
+                                                                         const uint32_t *__restrict__ list,
+                                                                         const uint32_t *__restrict__ count,
+                                                                         int64_t cap) {
+  __shared__ ExactLds<kListWaves> L;
+  const int wid = threadIdx.x >> 6;
+  const int lane = lsk::lane_id();
+  const int64_t c = (int64_t)count[0];
+  const int64_t total = c < cap ? c : cap;
+  for (int64_t i = blockIdx.x; i < total; i += gridDim.x) {
+    const int64_t qi = (int64_t)lsk::uniform(list[i]);
+    if (qi >= A.nq) continue;  // (uniform over the block)
+    const uint32_t ans = exact_kth<kListWaves>(A, qi, L, wid, lane);
+    if (wid == 0 && lane == 0) write_answer(A, qi, ans);
   }
 }
 
@@ -274,10 +303,15 @@ extern "C" int lsk_hip_knn_exact(const lsk_knn_args *args, const uint32_t *list,
   if (list && (!count || cap <= 0)) return 0;
   const int64_t work = list ? cap : (A.groups ? A.ngroups * lsk::kBucket : A.nq);
   if (work <= 0) return 0;
-  // persistent grid-stride loop: 2048 blocks x 4 waves (every wave exits at the end of
-  // the list; with an empty failure list the launch is a few microseconds)
-  const unsigned nblk = lsk_blocks(work, kWaves, 2048);
-  knn_exact_kernel<<<nblk, kWaves * 64, 0, (hipStream_t)stream>>>(A, list, count, cap);
+  // persistent grid-stride loops (every wave exits at the end of the list; with an empty
+  // failure list the launch is a few microseconds)
+  if (list) {
+    const unsigned nblk = lsk_blocks(work, 1, 1024);
+    knn_exact_list_kernel<<<nblk, kListWaves * 64, 0, (hipStream_t)stream>>>(A, list, count, cap);
+  } else {
+    const unsigned nblk = lsk_blocks(work, kWaves, 2048);
+    knn_exact_kernel<<<nblk, kWaves * 64, 0, (hipStream_t)stream>>>(A);
+  }
   LSK_CHECK_LAUNCH("knn_exact");
   return 0;
 }
