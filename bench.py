@@ -195,7 +195,7 @@ def main():
 
     # pipelined stream of point sets (see --pipeline): two different synthetic sets alternate
     # (auto: from 1e7 points; below that one HIP-graph replay per set is cheaper than the
-    # eager launches of the stream: 1e6 k=8 711 vs 702 Mpts/s, profiles/r2_s3_table)
+    # eager launches of the stream: 1e6 k=8 711 vs 702 Mpts/s, profiles/archive/r2_s3_table)
     pipelined = (args.pipeline == 1 or (args.pipeline < 0 and n_total >= PIPELINE_MIN_POINTS)) \
         and device.type == "cuda" and args.mode == "halo"
     host_sets = [make_points(n_total, rank, world, device, args.variant, d) for d in range(2 if pipelined else 1)]

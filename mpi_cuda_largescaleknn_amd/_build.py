@@ -69,7 +69,7 @@ FILE_FLAGS = {
     # the pass-1 log is a dynamically indexed private array: keep it in scratch memory
     # instead of promoting it to (dynamically indexed, hence many) VGPRs
     # max-memory-clause scheduling: 0.1255 vs 0.1265 s on 1e8 points, k=100 (ilp 0.131,
-    # iterative-ilp 0.138; same 72 VGPRs; profiles/r2_kernel/README.txt)
+    # iterative-ilp 0.138; same 72 VGPRs; profiles/archive/r2_kernel/README.txt)
     # candidates arrive in SGPRs: packed-math pairs would need them moved into VGPRs
     "knn_grid.hip": ["-fno-slp-vectorize"],
     "knn_rows.hip": ["-fno-slp-vectorize", "-mllvm", "-disable-promote-alloca-to-vector",

@@ -53,7 +53,7 @@ using lsk::fbits;
 
 // waves per workgroup: a block holds its LDS until its last wave ends, so 2-wave blocks
 // free slots sooner when waves differ in length (1B bench 633.5/633.9 vs 629.7/631.5
-// Mpts/s with 4; 1 wave per block is slower: profiles/r2_s3_wpb)
+// Mpts/s with 4; 1 wave per block is slower: profiles/archive/r2_s3_wpb)
 #ifndef LSK_ROWS_WPB
 #define LSK_ROWS_WPB 2
 #endif
@@ -67,7 +67,7 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 // 72 VGPRs with 4-candidate batches (its spills sit in per-pass code, not in the inner
 // loops). 1e8 pts, k=100 (round 1): 5 waves 0.166 s, 6 waves 0.149-0.152 s, 7 waves
 // 0.147 s, 8 waves (36 bins) 0.155 s; round 2: 8 waves 0.137 vs 7 waves 0.126 s. The
-// final kernel is VALU-issue bound (VALUBusy 74 %, profiles/r2_pmc_final).
+// final kernel is VALU-issue bound (VALUBusy 74 %, profiles/archive/r2_pmc_final).
 #define LSK_ROWS_MINW 7
 #endif
 // 40 bins of 1/8 octave of d² (kShift0) around the estimate (48 bins: 0.150 s at 6
@@ -103,7 +103,7 @@ constexpr int kPool = (kBins + 1) * 32;  // dwords per wave: histogram + trash r
 #define LSK_FILL_MIN 8
 #endif
 // Fixed design choices (each measured on 1e8 uniform points, k=100, one MI355X; the
-// alternatives were removed once rejected — profiles/r1_*, profiles/r2_kernel):
+// alternatives were removed once rejected — profiles/archive/r1_*, profiles/archive/r2_kernel):
 //  * best-first walk: inner nodes popped in order of their box distance to the centre of
 //    the wave's queries from a 64-entry priority list in two VGPRs, a DFS stack as
 //    bounded overflow (DFS by bucket-index gap 0.135 s, query-box key 0.129 s, centre

@@ -125,7 +125,7 @@ _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp
 # Largest single point-to-point message handed to the backend. RCCL 2.26 (torch 2.10's
 # librccl) corrupts the second half of any send/recv above 1 GiB (measured on MI355X with
 # a 1-rank group: 1024 MiB exact, 1025 MiB wrong from byte 2^29 on; all_to_all_single and
-# batch_isend_irecv alike; profiles/r2_rccl/README.txt). At 1B points on 2 ranks the
+# batch_isend_irecv alike; profiles/archive/r2_rccl/README.txt). At 1B points on 2 ranks the
 # redistribution sends ~3 GB to the peer, so every larger message is split into rounds of
 # at most this many bytes per peer.
 MAX_MSG_BYTES = int(os.environ.get("LSKNN_MAX_MSG_MB", "256")) << 20

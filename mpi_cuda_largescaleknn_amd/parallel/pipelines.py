@@ -95,7 +95,7 @@ def _hist_sample(n: int) -> int:
     if n < (1 << 20):
         return 1
     # at most ~8M sampled keys: their atomics into the shared histogram cost 2.6 ms per
-    # 500M-point rank at stride 8 (profiles/r1_v20/lb_scaling), and 8M samples already
+    # 500M-point rank at stride 8 (profiles/archive/r1_v20/lb_scaling), and 8M samples already
     # place the splitters far inside the 2 % tolerance
     return max(HIST_SAMPLE, n >> 23)
 
@@ -190,7 +190,7 @@ def redistribute(points: torch.Tensor, comm: Comm, box: torch.Tensor, info: RunI
 
 # points per host->device chunk of the streamed redistribution (env LSKNN_STREAM_CHUNK);
 # smaller chunks shorten the tail after the last copy (forced 1-rank RCCL, 1e8 points:
-# 32M / 16M / 8M -> 170.6 / 169.5 / 169.3 ms per step; profiles/r2_return)
+# 32M / 16M / 8M -> 170.6 / 169.5 / 169.3 ms per step; profiles/archive/r2_return)
 STREAM_CHUNK = int(os.environ.get("LSKNN_STREAM_CHUNK", str(1 << 24)))
 
 
@@ -630,7 +630,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
 # tree kernel only when it is slow enough per point, i.e. from k ~ 48 (the cell-grid
 # kernel is faster than the writes at k = 100: local_query keeps its output on the device) (1e8 uniform points on one
 # MI355X, step ms copy/direct: k=16 118/172, k=48 141/135, k=64 151/145, k=100
-# 176/170; 1e7 k=16 12.5/17.9; profiles/r1_v20/direct_out_ab.txt).
+# 176/170; 1e7 k=16 12.5/17.9; profiles/archive/r1_v20/direct_out_ab.txt).
 DIRECT_OUT_MIN_K = 48
 
 
@@ -669,7 +669,7 @@ FORCE_STREAM = os.environ.get("LSKNN_FORCE_STREAM", "0") == "1"
 # either way: keys only order the points. Off by default: on the 1B bench it hides the
 # 9 ms of bounds + keys but the chunked copies run slower than one 12 GB copy
 # (1583-1585 ms per step with one copy; 1595-1600 ms with 16M / 64M / 128M-point chunks;
-# profiles/r2_upload).
+# profiles/archive/r2_upload).
 UPLOAD_CHUNK = int(os.environ.get("LSKNN_UPLOAD_CHUNK", "0"))
 UPLOAD_MARGIN = 0.02
 _COPY_STREAMS: dict = {}

@@ -25,7 +25,7 @@ run one after the other (same results; used by the CPU tests).
 
 Measured on one MI355X (1B uniform, k=100, two alternating sets): 1414 ms per set
 (707.3 Mpts/s) vs 1573 ms (635.8) one set at a time; forced 1-rank RCCL group at 1e8:
-683 vs 599 Mpts/s (profiles/r2_s3_pipe, profiles/r2_s3_d2h).
+683 vs 599 Mpts/s (profiles/archive/r2_s3_pipe, profiles/archive/r2_s3_d2h).
 """
 from __future__ import annotations
 

@@ -16,7 +16,7 @@ DEV = torch.device("cuda", 0)
 g = torch.Generator(device="cuda").manual_seed(1)
 p = torch.rand((n, 3), generator=g, device="cuda")
 # kernel counters only on request: the stats build of the pass costs ~17 % (208 vs
-# 177 ms per 125M-point rank, profiles/r1_v20)
+# 177 ms per 125M-point rank, profiles/archive/r1_v20)
 cfg = E.KnnConfig(k=100, collect_stats="--stats" in sys.argv)
 
 
