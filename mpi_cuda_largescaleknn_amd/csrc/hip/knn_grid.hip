@@ -80,6 +80,9 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
+#ifndef LSK_GRID_SKIP1
+#define LSK_GRID_SKIP1 0
+#endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -370,6 +373,9 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
     for (int t = 0; t < 4; t++) {
       const uint32_t v = u[t];
       const bool in = v < hb;
+#if LSK_GRID_SKIP1
+      if (!__ballot(in)) continue;  // no lane counts this candidate (a uniform branch on VCC)
+#endif
       const uint32_t a = in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash;
       lds_add(a, inc);
       s.c_hi += in ? 1u : 0u;

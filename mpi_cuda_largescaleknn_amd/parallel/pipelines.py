@@ -531,10 +531,11 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
                   info: RunInfo, final_out: torch.Tensor, hook=None) -> torch.Tensor:
     """Local k-NN of every owned query + halo exchange + re-query (distributed runs).
     Returns the sorted d2; `final_out` receives the final distances (index.perm order).
-    `hook(after_stream) -> stream | None` (overlapped GPU path): called right after the
-    local k-NN is queued — independent work issued there (SetStream: the next point
-    set's redistribution) runs under the k-NN; the halo exchange is ordered after the
-    stream it returns."""
+    `hook(after) -> stream | None` (overlapped GPU path): called right after the local
+    k-NN is queued — independent work issued there (SetStream: the next point set's
+    redistribution) runs under the k-NN, ordered after `after` (a stream, or an event
+    recorded before the k-NN launch); the halo exchange / result return is ordered after
+    the stream it returns."""
     stats = info.stats if cfg.collect_stats else None
     gpu = K.is_gpu(index.pts)
     capturing = gpu and torch.cuda.is_current_stream_capturing()
@@ -543,10 +544,20 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         # result; the hook's work is issued right behind the k-NN launch, the failure
         # check after it
         pend: list = []
+        pre = None
+        if gpu and hook is not None:
+            # the hook's work is ordered after what precedes the k-NN (its collectives),
+            # not after the k-NN itself: it runs under it
+            pre = torch.cuda.Event()
+            pre.record(torch.cuda.current_stream(index.device))
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True,
                      deferred=None if capturing or not gpu else pend)
         if hook is not None:
-            hook(torch.cuda.current_stream(index.device) if gpu else None)
+            st = hook(pre)
+            if st is not None:
+                # the result return's collectives (queued on this stream next) follow the
+                # hook's: one communicator, never two collectives in flight
+                torch.cuda.current_stream(index.device).wait_stream(st)
         E.settle(pend)
         info.timer.mark("knn_local")
         return d2

@@ -367,7 +367,10 @@ class SetStream:
                     return None
                 # set j's redistribution under set i's k-NN (issued right after the k-NN
                 # launch), once set j's points are on the device
-                redist.wait_stream(after)
+                if isinstance(after, torch.cuda.Event):
+                    redist.wait_event(after)  # (a 1-rank group: the k-NN runs on `cur`)
+                else:
+                    redist.wait_stream(after)
                 redist.wait_stream(self.copy_stream)
                 with torch.cuda.stream(redist):
                     nxt["P"] = PL.redistribute_set(self._dbuf[j % 2], comm, cfg, n_totals[j])
