@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 7  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 8  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -76,7 +76,7 @@ class KnnArgs(C.Structure):
         ("stats", vp),
         ("qstatus", vp),
         ("seed", C.c_int32),
-        ("pad0", C.c_int32),
+        ("wave_base", C.c_int32),
         ("init_d2", vp),
         ("out_perm", vp),
         ("out_final", vp),
@@ -84,7 +84,7 @@ class KnnArgs(C.Structure):
         ("fail_count", vp),
         ("fail_cap", i64),
         ("debug_fail_mod", C.c_int32),
-        ("pad1", C.c_int32),
+        ("wave_end", C.c_int32),
         ("gate", vp),
         ("gate_on", C.c_int32),
         ("pad2", C.c_int32),

@@ -80,9 +80,6 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
-#ifndef LSK_GRID_SKIP1
-#define LSK_GRID_SKIP1 0
-#endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -95,10 +92,6 @@ constexpr uint32_t kShift0 = 20;          // 1/8 octave of d² per bin
 constexpr uint32_t kMaxPasses = 24;
 constexpr uint32_t kUnknown = 0xffffffffu;
 constexpr uint32_t kNaNBits = 0x7fc00000u;
-#ifndef LSK_GRID_EST_CALIB
-#define LSK_GRID_EST_CALIB 0.8f
-#endif
-constexpr float kEstCalib = LSK_GRID_EST_CALIB;  // first-range estimate scale (d²)
 
 // LSK_GRID_PROFILE builds (tuning only): shader-clock cycles per wave in candidate
 // processing / cell enumeration of each pass kind, and the whole wave, into
@@ -225,35 +218,6 @@ __device__ __forceinline__ float bcast64(float v, uint32_t j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
 }
 
-// 8-NN among the wave's own 64 queries, scaled to k (knn_rows own_group_estimate).
-__device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k,
-                                                     bool &dup) {
-  constexpr int M = 8;
-  float best[M];
-#pragma unroll
-  for (int i = 0; i < M; i++) best[i] = __builtin_inff();
-  for (uint32_t j0 = 0; j0 < nvalid; j0 += 8) {
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-      const uint32_t j = j0 + (uint32_t)t;
-      float v = lsk::dist2(s.qx - bcast64(s.qx, j), s.qy - bcast64(s.qy, j), s.qz - bcast64(s.qz, j));
-      v = (j < nvalid) ? v : __builtin_inff();
-#pragma unroll
-      for (int i = 0; i < M; i++) {
-        const float lo = fminf(best[i], v);
-        v = fmaxf(best[i], v);
-        best[i] = lo;
-      }
-    }
-  }
-  dup = best[1] == 0.f;
-  const uint32_t m0 = k < (uint32_t)M ? k : (uint32_t)M;
-  float dm = best[0];
-#pragma unroll
-  for (int i = 1; i < M; i++) dm = (i + 1 == (int)m0) ? best[i] : dm;
-  return dm * cbrtf(((float)k / (float)m0) * ((float)k / (float)m0));
-}
-
 __device__ void heap_sift(uint32_t *h, uint32_t i, uint32_t m) {
   const uint32_t v = h[i];
   for (;;) {
@@ -373,9 +337,6 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
     for (int t = 0; t < 4; t++) {
       const uint32_t v = u[t];
       const bool in = v < hb;
-#if LSK_GRID_SKIP1
-      if (!__ballot(in)) continue;  // no lane counts this candidate (a uniform branch on VCC)
-#endif
       const uint32_t a = in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash;
       lds_add(a, inc);
       s.c_hi += in ? 1u : 0u;
@@ -750,13 +711,14 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   const int lane = lsk::lane_id();
   if (!STRIDE) {
     const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
-    const uint64_t wave = (uint64_t)blk * kWPB + wid;
+    const uint64_t wave = (uint64_t)blk * kWPB + wid + (uint32_t)A.wave_base;
 #include "knn_grid_wave.inc"
   } else {
     if (A.gate && *A.gate != A.gate_on) return;
     uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
     if (A.groups && A.ngroups_dev) nwaves = min(nwaves, (uint64_t)*A.ngroups_dev);
-    for (uint64_t w = (uint64_t)blockIdx.x * kWPB + wid; w < nwaves; w += (uint64_t)gridDim.x * kWPB) {
+    if (A.wave_end > 0) nwaves = min(nwaves, (uint64_t)A.wave_end);
+    for (uint64_t w = (uint64_t)blockIdx.x * kWPB + wid + (uint32_t)A.wave_base; w < nwaves; w += (uint64_t)gridDim.x * kWPB) {
       [&](const uint64_t wave) {
 #include "knn_grid_wave.inc"
       }(w);
@@ -943,8 +905,10 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
     return 1;
   }
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
-  if (ngroups <= 0) return 0;
-  const unsigned nblk = lsk_blocks(ngroups, kWPB);
+  // this launch's waves: [wave_base, wave_end or ngroups)
+  const int64_t wend = A.wave_end > 0 && A.wave_end < ngroups ? A.wave_end : ngroups;
+  if (A.wave_base < 0 || wend - A.wave_base <= 0) return 0;
+  const unsigned nblk = lsk_blocks(wend - A.wave_base, kWPB);
   if (A.pad2 >= 1) {  // persistent strided form (see knn_grid_kernel); 2: a short list
     const unsigned cap = A.pad2 == 2 ? kStrideBlocksFull : kStrideBlocks;
     knn_grid_kernel<true><<<nblk < cap ? nblk : cap, kThreads, 0, (hipStream_t)stream>>>(A, *grid);

@@ -1051,13 +1051,14 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   const int lane = lsk::lane_id();
   if (!STRIDE) {
     const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
-    const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid;
+    const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid + (uint32_t)A.wave_base;
 #include "knn_rows_wave.inc"
   } else {
     if (A.gate && *A.gate != A.gate_on) return;
     uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
     if (A.groups && A.ngroups_dev) nwaves = min(nwaves, (uint64_t)*A.ngroups_dev);
-    for (uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid; w < nwaves;
+    if (A.wave_end > 0) nwaves = min(nwaves, (uint64_t)A.wave_end);
+    for (uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid + (uint32_t)A.wave_base; w < nwaves;
          w += (uint64_t)gridDim.x * kWavesPerBlock) {
       [&](const uint64_t wave) {
 #include "knn_rows_wave.inc"
@@ -1091,8 +1092,10 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
     }
   }
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
-  if (ngroups <= 0) return 0;
-  const unsigned nblk = lsk_blocks(ngroups, kWavesPerBlock);
+  // this launch's waves: [wave_base, wave_end or ngroups)
+  const int64_t wend = A.wave_end > 0 && A.wave_end < ngroups ? A.wave_end : ngroups;
+  if (A.wave_base < 0 || wend - A.wave_base <= 0) return 0;
+  const unsigned nblk = lsk_blocks(wend - A.wave_base, kWavesPerBlock);
   // Row work-queue capacity 32 entries per row: 5.6 KB of LDS per wave, 28 waves
   // per CU. One instance per tree count: the single-tree one (every local pass) has no
   // per-lane tree selects in its step loop; the two-tree one serves halo re-queries.

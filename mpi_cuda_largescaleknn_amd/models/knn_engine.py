@@ -426,7 +426,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
           stats: KnnStats | None = None, qstatus: torch.Tensor | None = None,
           init_d2: torch.Tensor | None = None, final_out: torch.Tensor | None = None,
           keep_d2: bool = False, deferred: list | None = None,
-          ngroups_dev: torch.Tensor | None = None, short_list: bool = False) -> torch.Tensor:
+          ngroups_dev: torch.Tensor | None = None, short_list: bool = False, chunks: int = 1) -> torch.Tensor:
     """k-th squared distance of every (or every listed group of) sorted query of
     `index` against index's tree (+ `extra`'s tree). Returns d2 in sorted order.
 
@@ -439,7 +439,8 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     host can queue other work (the overlapped halo exchange) behind it.
     `ngroups_dev` (with `groups`): the list's length as an int32 [1] tensor (on the GPU it
     stays on the device; `ngroups` is then the launch's upper bound); `short_list`: that
-    length is expected far below ngroups (kernels.knn_gpu)."""
+    length is expected far below ngroups; `chunks`: the pass as that many launches
+    (kernels.knn_gpu)."""
     n = index.n
     want_d2 = final_out is None or keep_d2 or out is not None
     if out is None and want_d2:
@@ -486,7 +487,7 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
                    grid=index.grid.view() if use_grid else None, ngroups_dev=ngroups_dev,
-                   expect_grid=GRID_EXPECT[0], short_list=short_list, **kw)
+                   expect_grid=GRID_EXPECT[0], short_list=short_list, chunks=chunks, **kw)
     gate = index.grid.gate if use_grid else None
     def check() -> bool:
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun

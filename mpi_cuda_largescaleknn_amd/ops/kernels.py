@@ -332,7 +332,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
             debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None,
-            expect_grid: bool = True, short_list: bool = False) -> FailWord:
+            expect_grid: bool = True, short_list: bool = False, chunks: int = 1) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -355,6 +355,10 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     ngroups (a rank's boundary groups): the kernel that runs takes its persistent strided
     form at full occupancy instead of one wave per possible group (most would be
     dispatched only to return: ~16 ms per 1M-block launch).
+    chunks > 1: the pass goes out as that many launches over consecutive wave ranges —
+    kernel boundaries at which the high-priority streams' kernels (the next set's
+    redistribution, the halo exchange) get CU slots: a running k-NN grid keeps every slot
+    until its last workgroup is dispatched.
     grid (impl "grid"): (slots, level, box, inf4[, gate]) of knn_engine.GridIndex — the
     cell-grid candidate source of knn_grid.hip for one tree whose points are the queries
     (same failure list and backstop as "rows"); with a device gate (int32 [1]) the grid
@@ -409,29 +413,36 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_count = _ptr(count)
     a.fail_cap = cap
     full = 2 if short_list and groups is not None and ngroups_dev is not None else 0
+    nw = ngroups if groups is not None else (nq + BUCKET - 1) // BUCKET
+    chunks = max(1, min(int(chunks), nw))
+    # the pass as `chunks` consecutive launches over wave ranges (0 = to the end)
+    spans = [(0, 0)] if chunks == 1 else [(nw * c // chunks, nw * (c + 1) // chunks) for c in range(chunks)]
     if impl == "grid":
         slots, level, gbox, inf4 = grid[:4]
         gate = grid[4] if len(grid) > 4 else None
         gv = GridView(_ptr(slots), None, _ptr(gbox), _ptr(inf4), int(level), 0)
-        if gate is not None:
-            # the device decides (lsk_hip_grid_decide): both kernels are queued, the one
-            # not chosen returns at its first instruction (no host read, graph-capturable)
-            a.gate = _ptr(gate)
-            a.gate_on = 1
-            a.pad2 = full if expect_grid else 1
-        else:
-            a.pad2 = full
-        check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
-        if gate is not None:
-            a.gate_on = 0
-            a.pad2 = 1 if expect_grid else full
-            check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
-        a.gate = None
-        a.pad2 = 0
+        for a.wave_base, a.wave_end in spans:
+            if gate is not None:
+                # the device decides (lsk_hip_grid_decide): both kernels are queued, the one
+                # not chosen returns at its first instruction (no host read, graph-capturable)
+                a.gate = _ptr(gate)
+                a.gate_on = 1
+                a.pad2 = full if expect_grid else 1
+            else:
+                a.pad2 = full
+            check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
+            if gate is not None:
+                a.gate_on = 0
+                a.pad2 = 1 if expect_grid else full
+                check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
+            a.gate = None
+            a.pad2 = 0
     else:
-        a.pad2 = full
-        check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
-        a.pad2 = 0
+        for a.wave_base, a.wave_end in spans:
+            a.pad2 = full
+            check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
+            a.pad2 = 0
+    a.wave_base = a.wave_end = 0
     # exact backstop over the failure list (device-side count: empty list = short no-op)
     check(lib.lsk_hip_knn_exact(C.byref(a), _ptr(flist), _ptr(count), cap, st), "knn_exact")
     return FailWord(count, cap)

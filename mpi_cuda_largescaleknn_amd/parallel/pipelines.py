@@ -551,7 +551,8 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
             pre = torch.cuda.Event()
             pre.record(torch.cuda.current_stream(index.device))
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True,
-                     deferred=None if capturing or not gpu else pend)
+                     deferred=None if capturing or not gpu else pend,
+                     chunks=KNN_CHUNKS if hook is not None else 1)
         if hook is not None:
             st = hook(pre)
             if st is not None:
@@ -607,7 +608,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         if not gpu:
             recv = _halo_send(index, radii, comm, cfg, info, marks=False)
         E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=ilist, ngroups=ng,
-                ngroups_dev=icnt, deferred=pend if gpu else None)
+                ngroups_dev=icnt, deferred=pend if gpu else None, chunks=KNN_CHUNKS if gpu else 1)
     if gpu:
         if hook is not None:
             # independent work under the k-NN (SetStream: the next set's redistribution);
@@ -663,6 +664,12 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
     return out
 
 
+
+# Passes with work of other streams to run beside them (the next set's redistribution,
+# the halo exchange) go out as this many launches: a running k-NN grid holds every CU slot
+# until its last workgroup is dispatched, so a high-priority stream's kernels only start
+# at a kernel boundary (env LSKNN_KNN_CHUNKS; 1 = one launch).
+KNN_CHUNKS = int(os.environ.get("LSKNN_KNN_CHUNKS", "4"))
 
 # A 1-rank group (forced multi-rank runs) has no peer, hence no halo: knn_with_halo skips
 # the publish / filter / exchange / re-query. True: run them anyway (the RCCL call-site

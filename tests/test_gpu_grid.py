@@ -241,3 +241,33 @@ def test_short_group_list_strided_launch(gen, monkeypatch):
     mask = torch.ones(idx.n, dtype=torch.bool)
     mask[rows] = False
     assert bool((d2.cpu()[mask] == -7.0).all())
+
+
+@pytest.mark.parametrize("gen", ["uniform", "mixed_scale"])
+def test_chunked_pass_equals_one_launch(gen, monkeypatch):
+    """A pass sent as several launches over consecutive wave ranges (chunks: kernel
+    boundaries for the high-priority streams) gives exactly the one-launch result — the
+    whole set, and a device-counted group list — on the grid (uniform) and rows (mixed-
+    scale: the gate picks knn_rows) kernels."""
+    monkeypatch.setattr(E, "GRID", "auto")
+    p = GENERATORS[gen](150_001, seed=8)
+    idx = E.build_index(p.to(DEV), grid=True)
+    cfg = E.KnnConfig(k=32)
+    hint2 = E.radius_hint(idx.box, idx.n, 32)
+    one = E.query(idx, cfg, hint2)
+    for c in (2, 3, 7):
+        assert torch.equal(E.query(idx, cfg, hint2, chunks=c), one), c
+    ng = (idx.n + 63) // 64
+    lst = torch.arange(0, ng, 3, dtype=torch.int32)
+    cnt = torch.tensor([lst.numel() - 5], dtype=torch.int32)
+    full = torch.full((ng,), -1, dtype=torch.int32)
+    full[:lst.numel()] = lst
+    outs = []
+    for c in (1, 4):
+        d2 = torch.zeros(idx.n, device=DEV)
+        E.query(idx, cfg, hint2, out=d2, groups=full.to(DEV), ngroups=ng, ngroups_dev=cnt.to(DEV), chunks=c)
+        outs.append(d2)
+    assert torch.equal(outs[0], outs[1])
+    rows = (lst[:cnt.item()].long()[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
+    rows = rows[rows < idx.n]
+    assert torch.equal(outs[1].cpu()[rows], one.cpu()[rows])
