@@ -669,7 +669,7 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
 # the halo exchange) go out as this many launches: a running k-NN grid holds every CU slot
 # until its last workgroup is dispatched, so a high-priority stream's kernels only start
 # at a kernel boundary (env LSKNN_KNN_CHUNKS; 1 = one launch).
-KNN_CHUNKS = int(os.environ.get("LSKNN_KNN_CHUNKS", "4"))
+KNN_CHUNKS = int(os.environ.get("LSKNN_KNN_CHUNKS", "1"))
 
 # A 1-rank group (forced multi-rank runs) has no peer, hence no halo: knn_with_halo skips
 # the publish / filter / exchange / re-query. True: run them anyway (the RCCL call-site

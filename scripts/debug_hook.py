@@ -38,6 +38,44 @@ def wrap(mod, name):
 
 
 wrap(E, "query")
+POLL = []
+
+
+def poll_events(tagged):
+    """Background thread: host time at which each (tag, event) completes."""
+    import threading
+
+    def run():
+        pending = list(tagged)
+        while pending:
+            for item in list(pending):
+                if item[1].query():
+                    LOG.append((time.perf_counter() - T0, f"   done {item[0]}", None))
+                    pending.remove(item)
+            time.sleep(0.0002)
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    POLL.append(th)
+
+
+_rs = PL.redistribute_set
+
+
+def redistribute_set(*a, **kw):
+    # events at entry: the redistribution stream (after its waits), the copy stream, and the
+    # compute stream (after the k-NN just queued)
+    st = {}
+    for nm, s_ in (("redist(entry)", torch.cuda.current_stream(dev)), ("copy", RUNNER[0].copy_stream),
+                   ("compute", torch.cuda.default_stream(dev))):
+        e = torch.cuda.Event()
+        e.record(s_)
+        st[nm] = e
+    poll_events(list(st.items()))
+    return _rs(*a, **kw)
+
+
+PL.redistribute_set = redistribute_set
+RUNNER = []
 wrap(PL, "redistribute_set")
 wrap(K.FailWord, "stage")
 wrap(K.FailWord, "value")
@@ -50,12 +88,13 @@ for s in range(2):
     sets.append(torch.rand((n, 3), generator=g).pin_memory())
 outs = [torch.empty(n, dtype=torch.float32).pin_memory() for _ in range(2)]
 runner = SetStream(comm, E.KnnConfig(k=100), direct_out=False)
+RUNNER.append(runner)
 runner.run([sets[i % 2] for i in range(3)], [outs[i % 2] for i in range(3)], n_totals=[n] * 3)
 torch.cuda.synchronize()
 LOG.clear()
 T0 = time.perf_counter()
 runner.run([sets[i % 2] for i in range(5)], [outs[i % 2] for i in range(5)], n_totals=[n] * 5)
 torch.cuda.synchronize()
-for t, tag, idle in LOG:
-    print(f"{t * 1e3:9.2f} ms  {'idle' if idle else 'busy'}  {tag}")
+for t, tag, idle in sorted(LOG, key=lambda x: x[0]):
+    print(f"{t * 1e3:9.2f} ms  {'' if idle is None else ('idle' if idle else 'busy')}  {tag}")
 LA.finalize(launch)
