@@ -83,6 +83,7 @@ class SetStream:
             # high priority: its kernels get CU slots as the k-NN grid's workgroups retire
             self.redist_stream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
         self._dbuf: list[torch.Tensor | None] = [None, None]
+        self._copy_ev: dict = {}  # set index -> event right behind its upload
         self.last_info: PL.RunInfo | None = None
 
     def _buffer(self, slot: int, like: torch.Tensor) -> torch.Tensor:
@@ -98,6 +99,25 @@ class SetStream:
         self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.copy_stream):
             self._buffer(j % 2, host).copy_(host, non_blocking=True)
+        self._mark_copy(j)
+
+    def _mark_copy(self, j: int) -> None:
+        # an event right behind set j's upload: consumers wait for THAT, not for a marker
+        # placed on the copy stream later — with 4 hardware queues per process the copy
+        # stream shares one with the output stream, whose result copy (a blit kernel) gets
+        # no CU slot while a k-NN grid is being dispatched, and a later marker would sit
+        # behind it (the next set's redistribution then started only after the k-NN)
+        ev = torch.cuda.Event()
+        ev.record(self.copy_stream)
+        self._copy_ev[j] = ev
+
+    def _uploaded(self, stream, j: int) -> None:
+        """`stream` waits for set j's upload."""
+        ev = self._copy_ev.pop(j, None)
+        if ev is not None:
+            stream.wait_event(ev)
+        else:
+            stream.wait_stream(self.copy_stream)
 
     def run(self, inputs: Sequence[torch.Tensor], outputs: Sequence[torch.Tensor],
             n_totals: Sequence[int | None] | None = None,
@@ -149,7 +169,7 @@ class SetStream:
         # is queued; set i's output copy follows that check (a rerun rewrites the output)
         prev = None  # set i-1: see _query
         for i in range(n):
-            cur.wait_stream(self.copy_stream)  # set i's points are on the device
+            self._uploaded(cur, i)  # set i's points are on the device
             pts = self._dbuf[i % 2]
             if i + 1 < n:
                 self._prefetch(i + 1, inputs[i + 1])
@@ -222,7 +242,7 @@ class SetStream:
 
         def build(j: int):
             # set j's points are on the device (copy stream), then its index on `side`
-            side.wait_stream(self.copy_stream)
+            self._uploaded(side, j)
             info = new_info()
             info.timer.start()
             with torch.cuda.stream(side):
@@ -271,6 +291,7 @@ class SetStream:
             self.copy_stream.wait_event(ev)
         with torch.cuda.stream(self.copy_stream):
             self._buffer(j % 2, host).copy_(host, non_blocking=True)
+        self._mark_copy(j)
 
     def _run_prepartitioned(self, inputs, outputs, new_info, done) -> None:
         """Several ranks, one file per rank and set: set i+1's upload runs under set i
@@ -284,7 +305,7 @@ class SetStream:
         copies: list = []
         prev = None
         for i in range(n):
-            cur.wait_stream(self.copy_stream)  # set i's points are on the device
+            self._uploaded(cur, i)  # set i's points are on the device
             pts = self._dbuf[i % 2]
             if i + 1 < n:
                 self._prefetch(i + 1, inputs[i + 1])  # after set i-1's reads of that buffer
@@ -336,7 +357,7 @@ class SetStream:
             return
         red_ev: list = [None, None]  # event after the redistribution that read input buffer b
         self._prefetch(0, inputs[0])
-        cur.wait_stream(self.copy_stream)
+        self._uploaded(cur, 0)
         P = PL.redistribute_set(self._dbuf[0], comm, cfg, n_totals[0], new_info())
         red_ev[0] = torch.cuda.Event()
         red_ev[0].record(cur)
@@ -371,7 +392,7 @@ class SetStream:
                     redist.wait_event(after)  # (a 1-rank group: the k-NN runs on `cur`)
                 else:
                     redist.wait_stream(after)
-                redist.wait_stream(self.copy_stream)
+                self._uploaded(redist, j)
                 with torch.cuda.stream(redist):
                     nxt["P"] = PL.redistribute_set(self._dbuf[j % 2], comm, cfg, n_totals[j])
                     e = torch.cuda.Event()
