@@ -544,17 +544,14 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         # result; the hook's work is issued right behind the k-NN launch, the failure
         # check after it
         pend: list = []
-        pre = None
-        if gpu and hook is not None:
-            # the hook's work is ordered after what precedes the k-NN (its collectives),
-            # not after the k-NN itself: it runs under it
-            pre = torch.cuda.Event()
-            pre.record(torch.cuda.current_stream(index.device))
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True,
                      deferred=None if capturing or not gpu else pend,
                      chunks=KNN_CHUNKS if hook is not None else 1)
         if hook is not None:
-            st = hook(pre)
+            # the hook's work follows the k-NN: run beside it, the next set's redistribution
+            # kernels slowed it by more than they took (1e8 forced 1-rank RCCL stream:
+            # 854 vs 979 Mpts/s, profiles/r4_s1/fd_k_c1.log)
+            st = hook(torch.cuda.current_stream(index.device) if gpu else None)
             if st is not None:
                 # the result return's collectives (queued on this stream next) follow the
                 # hook's: one communicator, never two collectives in flight
@@ -609,11 +606,17 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
             recv = _halo_send(index, radii, comm, cfg, info, marks=False)
         E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=ilist, ngroups=ng,
                 ngroups_dev=icnt, deferred=pend if gpu else None, chunks=KNN_CHUNKS if gpu else 1)
+        if gpu:
+            ev_int = torch.cuda.Event()
+            ev_int.record(comp)
     if gpu:
         if hook is not None:
-            # independent work under the k-NN (SetStream: the next set's redistribution);
-            # the halo collectives follow its collectives (one communicator: never two in
-            # flight)
+            # independent work (SetStream: the next set's redistribution), after the
+            # interior pass: kernels issued while a k-NN grid is dispatched only get CU
+            # slots once it is, and run beside it they cost it more than they take (see the
+            # one-rank branch above); the halo exchange follows the hook's collectives (one
+            # communicator: never two in flight)
+            cur.wait_event(ev_int)
             st = hook(cur)
             if st is not None:
                 side.wait_stream(st)
