@@ -544,14 +544,16 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         # result; the hook's work is issued right behind the k-NN launch, the failure
         # check after it
         pend: list = []
+        pre = None
+        if gpu and hook is not None and REDIST_UNDER_KNN:
+            pre = torch.cuda.Event()
+            pre.record(torch.cuda.current_stream(index.device))
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True,
                      deferred=None if capturing or not gpu else pend,
                      chunks=KNN_CHUNKS if hook is not None else 1)
         if hook is not None:
-            # the hook's work follows the k-NN: run beside it, the next set's redistribution
-            # kernels slowed it by more than they took (1e8 forced 1-rank RCCL stream:
-            # 854 vs 979 Mpts/s, profiles/r4_s1/fd_k_c1.log)
-            st = hook(torch.cuda.current_stream(index.device) if gpu else None)
+            # the hook's work follows the k-NN (REDIST_UNDER_KNN: only what precedes it)
+            st = hook(pre if pre is not None else (torch.cuda.current_stream(index.device) if gpu else None))
             if st is not None:
                 # the result return's collectives (queued on this stream next) follow the
                 # hook's: one communicator, never two collectives in flight
@@ -616,7 +618,8 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
             # slots once it is, and run beside it they cost it more than they take (see the
             # one-rank branch above); the halo exchange follows the hook's collectives (one
             # communicator: never two in flight)
-            cur.wait_event(ev_int)
+            if not REDIST_UNDER_KNN:
+                cur.wait_event(ev_int)
             st = hook(cur)
             if st is not None:
                 side.wait_stream(st)
@@ -673,6 +676,10 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
 # until its last workgroup is dispatched, so a high-priority stream's kernels only start
 # at a kernel boundary (env LSKNN_KNN_CHUNKS; 1 = one launch).
 KNN_CHUNKS = int(os.environ.get("LSKNN_KNN_CHUNKS", "1"))
+# The next set's redistribution (SetStream's hook) is ordered after the local k-NN; 1: only
+# after what precedes the k-NN launch, so that it may run beside it (env
+# LSKNN_REDIST_UNDER_KNN; see profiles/r4_s1/README.md for the measurements)
+REDIST_UNDER_KNN = os.environ.get("LSKNN_REDIST_UNDER_KNN", "0") == "1"
 
 # A 1-rank group (forced multi-rank runs) has no peer, hence no halo: knn_with_halo skips
 # the publish / filter / exchange / re-query. True: run them anyway (the RCCL call-site
