@@ -38,7 +38,11 @@ import os
 import sys
 import time
 
-import torch
+# hardware queues per process: the HIP runtime reads this when torch loads it, so before
+# `import torch` (see mpi_cuda_largescaleknn_amd/__init__.py)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -9,8 +9,8 @@ __version__ = "0.1.0"
 
 import os as _os
 
-# Hardware queues per process (read by the HIP runtime when the GPU is first used: import
-# this package before that). HIP's default of 4 is fewer than the streams a stream of
+# Hardware queues per process (read by the HIP runtime when it is loaded, i.e. at
+# `import torch`: import this package first, or set it in the environment — bench.py does). HIP's default of 4 is fewer than the streams a stream of
 # point sets keeps busy (compute, copy, output, redistribution, halo, RCCL's): unrelated
 # streams then share an in-order queue and wait for each other — the forced 1-rank RCCL
 # 1e8 stream ran at 844.8 Mpts/s with 4 queues, 977.4 with 8, 973.5 with 16
