@@ -39,8 +39,9 @@ import sys
 import time
 
 # hardware queues per process: the HIP runtime reads this when torch loads it, so before
-# `import torch` (see mpi_cuda_largescaleknn_amd/__init__.py)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# `import torch` (at least 8, see mpi_cuda_largescaleknn_amd/__init__.py)
+_hwq = max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4), int(os.environ.get("LSKNN_HW_QUEUES", "8")))
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(_hwq, 32))
 
 import torch  # noqa: E402
 

@@ -14,7 +14,9 @@ import os as _os
 # point sets keeps busy (compute, copy, output, redistribution, halo, RCCL's): unrelated
 # streams then share an in-order queue and wait for each other — the forced 1-rank RCCL
 # 1e8 stream ran at 844.8 Mpts/s with 4 queues, 977.4 with 8, 973.5 with 16
-# (profiles/r4_s1/fd_q*.log). A value set by the user is kept.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# (profiles/r4_s1/fd_q*.log). Raised to at least LSKNN_HW_QUEUES (default 8; never above
+# 32); a larger value already in the environment is kept.
+_hwq = max(int(_os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4), int(_os.environ.get("LSKNN_HW_QUEUES", "8")))
+_os.environ["GPU_MAX_HW_QUEUES"] = str(min(_hwq, 32))
 
 from .models.knn_engine import KnnConfig, build_index, knn_distances, query  # noqa: F401
