@@ -552,7 +552,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
                      deferred=None if capturing or not gpu else pend,
                      chunks=KNN_CHUNKS if hook is not None else 1)
         if hook is not None:
-            # the hook's work follows the k-NN (REDIST_UNDER_KNN: only what precedes it)
+            # the hook's work follows what precedes the k-NN (REDIST_UNDER_KNN), else the k-NN
             st = hook(pre if pre is not None else (torch.cuda.current_stream(index.device) if gpu else None))
             if st is not None:
                 # the result return's collectives (queued on this stream next) follow the
@@ -613,11 +613,9 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
             ev_int.record(comp)
     if gpu:
         if hook is not None:
-            # independent work (SetStream: the next set's redistribution), after the
-            # interior pass: kernels issued while a k-NN grid is dispatched only get CU
-            # slots once it is, and run beside it they cost it more than they take (see the
-            # one-rank branch above); the halo exchange follows the hook's collectives (one
-            # communicator: never two in flight)
+            # independent work (SetStream: the next set's redistribution) beside the
+            # interior pass (REDIST_UNDER_KNN, else after it); the halo exchange follows
+            # the hook's collectives (one communicator: never two in flight)
             if not REDIST_UNDER_KNN:
                 cur.wait_event(ev_int)
             st = hook(cur)
@@ -676,10 +674,12 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
 # until its last workgroup is dispatched, so a high-priority stream's kernels only start
 # at a kernel boundary (env LSKNN_KNN_CHUNKS; 1 = one launch).
 KNN_CHUNKS = int(os.environ.get("LSKNN_KNN_CHUNKS", "1"))
-# The next set's redistribution (SetStream's hook) is ordered after the local k-NN; 1: only
-# after what precedes the k-NN launch, so that it may run beside it (env
-# LSKNN_REDIST_UNDER_KNN; see profiles/r4_s1/README.md for the measurements)
-REDIST_UNDER_KNN = os.environ.get("LSKNN_REDIST_UNDER_KNN", "0") == "1"
+# The next set's redistribution (SetStream's hook) is ordered after what precedes the local
+# k-NN launch, so it runs beside the k-NN once its upload has landed (forced 1-rank RCCL
+# 1e8 stream with 8 hardware queues: 997.4 vs 980.5 Mpts/s ordered after the k-NN;
+# with 4 shared queues it had measured slower, profiles/r4_s1/fd_o_*.log); 0: after the
+# k-NN (env LSKNN_REDIST_UNDER_KNN)
+REDIST_UNDER_KNN = os.environ.get("LSKNN_REDIST_UNDER_KNN", "1") == "1"
 
 # A 1-rank group (forced multi-rank runs) has no peer, hence no halo: knn_with_halo skips
 # the publish / filter / exchange / re-query. True: run them anyway (the RCCL call-site
