@@ -241,3 +241,17 @@ def test_ref_memory_arithmetic():
     RA.check_ref_fits(125_000_000, 100, 288 * 10**9, 8)
     with pytest.raises(ValueError, match="at least 3 ranks"):
         RA.check_ref_fits(1_000_000_000, 100, 288 * 10**9, 1)
+
+
+@pytest.mark.parametrize("env,want", [(None, "8"), ("4", "8"), ("16", "16"), ("64", "32")])
+def test_hardware_queue_floor(env, want):
+    """Importing the package (bench.py does the same before `import torch`) raises the HIP
+    hardware-queue count to at least 8 — the box's 4 made unrelated streams share in-order
+    queues — keeps a larger setting and never exceeds 32."""
+    e = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "LSKNN_HW_QUEUES")}
+    if env is not None:
+        e["GPU_MAX_HW_QUEUES"] = env
+    out = subprocess.run([sys.executable, "-c", "import os, mpi_cuda_largescaleknn_amd; "
+                          "print(os.environ['GPU_MAX_HW_QUEUES'])"], cwd=ROOT, env=e,
+                         capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == want
