@@ -18,7 +18,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / lsk::kWave;
 constexpr int kRadix = 256;
-constexpr int kRows = 16;                              // rows of 64 per wave per tile
+constexpr int kRows = 16;  // rows of 64 per wave per tile (8: 36.5 vs 33.6 ms for 1B keys)
 constexpr int kTile = kWaves * lsk::kWave * kRows;     // 4096 elements
 constexpr unsigned kMaxBlocks = 2048;
 

@@ -1,0 +1,38 @@
+"""Index-build pieces alone on N uniform points: curve keys, 4-pass key sort (iota values),
+key census, gather, tree, grid; best of 3 each (events).
+
+    python scripts/sort_bench.py [N]"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from mpi_cuda_largescaleknn_amd.models import knn_engine as E  # noqa: E402
+from mpi_cuda_largescaleknn_amd.ops import kernels as K  # noqa: E402
+
+n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_000_000_000
+g = torch.Generator(device="cuda").manual_seed(1)
+p = torch.rand((n, 3), generator=g, device="cuda")
+box = K.bounds(p)
+
+
+def t(fn, reps=3):
+    best, out = 1e9, None
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        out = fn()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b))
+    return out, best
+
+
+(keys,), t_keys = t(lambda: (K.morton(p, box, with_iota=False)[0],))
+(sk, perm), t_sort = t(lambda: K.sort_keys_iota(keys, 30))
+_, t_census = t(lambda: K.key_census(sk[:n], E.HEAVY_RUN))
+pts, t_gather = t(lambda: K.gather3(p, perm, pad=K.PAD_POINTS))
+_, t_build = t(lambda: E.build_index(p, box, grid=True))
+print(f"n={n}: keys {t_keys:.2f} ms, sort {t_sort:.2f} ms, census {t_census:.2f} ms, gather {t_gather:.2f} ms, "
+      f"whole build_index {t_build:.2f} ms", flush=True)
