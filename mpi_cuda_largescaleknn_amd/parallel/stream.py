@@ -44,6 +44,10 @@ from .comm import Comm
 # (measured slower: 1B k=100 1168 vs 1106 ms per set; the build's workgroups hold CU slots
 # among the k-NN's far longer than the build takes alone — kept as an option)
 BUILD_AHEAD = os.environ.get("LSKNN_BUILD_AHEAD", "0") != "0"
+# One rank: set i-1's result copy to host (device->host PCIe traffic slows whatever runs
+# beside it) is queued behind set i's index build, i.e. beside set i's k-NN, instead of
+# beside the build (env LSKNN_OUT_AFTER_BUILD; A/B in profiles/r4_final/README.md)
+OUT_AFTER_BUILD = os.environ.get("LSKNN_OUT_AFTER_BUILD", "0") == "1"
 
 
 def _index_tensors(index: E.LocalIndex):
@@ -177,7 +181,12 @@ class SetStream:
             with trace.range(f"lsknn:set {i}"):
                 info.timer.start()
                 index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info)
-                rel = self._release(prev, outputs) if prev is not None else None
+                after = None
+                if OUT_AFTER_BUILD and prev is not None:
+                    # set i-1's result copy beside set i's k-NN rather than its build
+                    after = torch.cuda.Event()
+                    after.record(cur)
+                rel = self._release(prev, outputs, after) if prev is not None else None
                 rec = self._query(i, index, hint2, info, outputs)
                 del index
             if rel is not None:  # set i-1's output, waited for once set i's k-NN is queued
@@ -205,7 +214,7 @@ class SetStream:
         ev.synchronize()
         done(j)
 
-    def _release(self, rec, outputs):
+    def _release(self, rec, outputs, after=None):
         """Set j: its failure check (a 4-byte read behind its k-NN), then its device result
         to host on the output stream (behind its k-NN, or behind everything queued so far
         when the check queued a rerun). Returns (j, event after which outputs[j] is in
@@ -217,6 +226,8 @@ class SetStream:
             ev.record(cur)
         if res is not None:
             self.out_stream.wait_event(ev)
+            if after is not None:
+                self.out_stream.wait_event(after)
             with torch.cuda.stream(self.out_stream):
                 outputs[j].copy_(res, non_blocking=True)
                 ev = torch.cuda.Event()
