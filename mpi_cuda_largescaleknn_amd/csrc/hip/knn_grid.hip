@@ -80,6 +80,13 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
+#ifndef LSK_GRID_NETSEL
+#define LSK_GRID_NETSEL 0  // (A/B) 1: band selection by a sorting network for bands of <= kNet values
+#endif
+#ifndef LSK_GRID_NET
+#define LSK_GRID_NET 32
+#endif
+constexpr int kNet = LSK_GRID_NET;
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
