@@ -84,6 +84,7 @@ __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
 // 0.082 -> 0.079 s against the LDS heap for every band; 16 values: no gain, bands of
 // 17..32 then take the heap and the wave runs both)
 constexpr int kNet = 32;
+constexpr int kNetMin = 8;  // the network serves a wave only if some band holds more values
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
