@@ -62,9 +62,6 @@ constexpr int kThreads = kWavesPerBlock * lsk::kWave;
 #ifndef LSK_ROWS_BINS
 #define LSK_ROWS_BINS 40
 #endif
-#ifndef LSK_ROWS_NETSEL
-#define LSK_ROWS_NETSEL 0  // (A/B) 1: band selection by a sorting network (knn_grid's)
-#endif
 #ifndef LSK_ROWS_MINW
 // 7 waves/SIMD: 40 bins keep the LDS at 5.6 KB per wave (28 waves/CU) and the allocator fits
 // 72 VGPRs with 4-candidate batches (its spills sit in per-pass code, not in the inner
