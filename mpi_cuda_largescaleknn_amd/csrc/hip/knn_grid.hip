@@ -85,9 +85,6 @@ __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
 // 17..32 then take the heap and the wave runs both)
 constexpr int kNet = 32;
 constexpr int kNetMin = 8;  // the network serves a wave only if some band holds more values
-#ifndef LSK_GRID_SHRINK4
-#define LSK_GRID_SHRINK4 0  // (A/B) 1: hist_shrink reads four top rows at once
-#endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -173,29 +170,6 @@ __device__ __forceinline__ void underflow_restart(Lane &s) {
 
 // Drop top bins while at least k counted values stay below: the lane's bound shrinks.
 __device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
-#if LSK_GRID_SHRINK4
-  // the next four top rows are read at once (independent LDS reads instead of a chain)
-  bool more = s.bin_hi > 0;
-  while (more) {
-    const int32_t b = s.bin_hi;
-    uint32_t t[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) t[i] = b - 1 - i >= 0 ? hist_read(pool, (uint32_t)(b - 1 - i), lane) : 0u;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (more) {
-        if (s.bin_hi <= 0 || s.c_hi - t[i] < k) {
-          more = false;
-        } else {
-          s.c_hi -= t[i];
-          s.bin_hi--;
-        }
-      }
-    }
-    s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
-    more = more && s.bin_hi > 0;
-  }
-#else
   while (s.bin_hi > 0) {
     const uint32_t top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
     if (s.c_hi - top < k) break;
@@ -203,7 +177,6 @@ __device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int l
     s.bin_hi--;
     s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
   }
-#endif
   // k exact zeros: the k-th is 0 and nothing can be closer (knn_rows zero probe)
   if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
 }
