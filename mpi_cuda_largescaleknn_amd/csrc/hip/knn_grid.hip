@@ -85,9 +85,6 @@ __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
 // 17..32 then take the heap and the wave runs both)
 constexpr int kNet = 32;
 constexpr int kNetMin = 8;  // the network serves a wave only if some band holds more values
-#ifndef LSK_GRID_BFCOLLECT
-#define LSK_GRID_BFCOLLECT 0  // (A/B) 1: branch-free collect appends (one spare slot per lane)
-#endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -354,19 +351,6 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
     const bool any = (u0 - bl < bw) || (u1 - bl < bw) || (u2 - bl < bw) || (u3 - bl < bw);
     if (!__ballot(any)) return;
     const uint32_t u[4] = {u0, u1, u2, u3};
-#if LSK_GRID_BFCOLLECT
-    // branch-free: every candidate is written, to the lane's next slot when it is in the
-    // band, else to the lane's spare slot (bc, allocated with the pool offsets) — no exec
-    // round trips; a count past bc is a mismatch (the values then stop at the spare slot)
-    const uint32_t base = lds_addr(pool) + s.coff * 4u;
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const bool in = u[t] - bl < bw;
-      const uint32_t slot = in ? min(s.ccnt, s.bc) : s.bc;
-      *(lds_u32 *)(uintptr_t)(base + slot * 4u) = u[t];
-      s.ccnt += in ? 1u : 0u;
-    }
-#else
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       if (u[t] - bl < bw) {
@@ -374,7 +358,6 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
         s.ccnt++;
       }
     }
-#endif
   }
 }
 
