@@ -85,9 +85,6 @@ __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
 // 17..32 then take the heap and the wave runs both)
 constexpr int kNet = 32;
 constexpr int kNetMin = 8;  // the network serves a wave only if some band holds more values
-#ifndef LSK_GRID_FLATCOLLECT
-#define LSK_GRID_FLATCOLLECT 0  // (A/B) 1: collect appends under one exec branch
-#endif
 #ifndef LSK_GRID_TOPBINS
 #define LSK_GRID_TOPBINS 10
 #endif
@@ -354,14 +351,6 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
     const bool any = (u0 - bl < bw) || (u1 - bl < bw) || (u2 - bl < bw) || (u3 - bl < bw);
     if (!__ballot(any)) return;
     const uint32_t u[4] = {u0, u1, u2, u3};
-#if LSK_GRID_FLATCOLLECT
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const bool in = u[t] - bl < bw;
-      if (in && s.ccnt < s.bc) pool[s.coff + s.ccnt] = u[t];  // one exec branch
-      s.ccnt += in ? 1u : 0u;
-    }
-#else
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       if (u[t] - bl < bw) {
@@ -369,7 +358,6 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
         s.ccnt++;
       }
     }
-#endif
   }
 }
 
