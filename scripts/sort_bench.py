@@ -16,13 +16,15 @@ p = torch.rand((n, 3), generator=g, device="cuda")
 box = K.bounds(p)
 
 
-def t(fn, reps=3):
+def t(fn, reps=3, setup=None):
+    """Best of `reps` event-timed calls; `setup()` (untimed) makes each call's fresh input."""
     best, out = 1e9, None
     for _ in range(reps):
+        arg = setup() if setup is not None else None
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         a.record()
-        out = fn()
+        out = fn(arg) if setup is not None else fn()
         b.record()
         b.synchronize()
         best = min(best, a.elapsed_time(b))
@@ -30,7 +32,10 @@ def t(fn, reps=3):
 
 
 (keys,), t_keys = t(lambda: (K.morton(p, box, with_iota=False)[0],))
-(sk, perm), t_sort = t(lambda: K.sort_keys_iota(keys, 30))
+# the sort ping-pongs through its input buffer (an even pass count leaves the sorted keys
+# there): every rep sorts a fresh copy of the unsorted keys, or reps 2-3 would sort sorted
+# keys and the gather below would read an identity permutation
+(sk, perm), t_sort = t(lambda kk: K.sort_keys_iota(kk, 30), setup=lambda: keys.clone())
 _, t_census = t(lambda: K.key_census(sk[:n], E.HEAVY_RUN))
 pts, t_gather = t(lambda: K.gather3(p, perm, pad=K.PAD_POINTS))
 _, t_build = t(lambda: E.build_index(p, box, grid=True))
