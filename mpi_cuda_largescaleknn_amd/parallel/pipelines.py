@@ -755,19 +755,16 @@ def upload_keyed(host_pts: torch.Tensor, dev: torch.device, chunk: int | None = 
 
 
 def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
-                info: RunInfo | None = None, pre: tuple | None = None) -> tuple[E.LocalIndex, float | torch.Tensor]:
+                info: RunInfo | None = None) -> tuple[E.LocalIndex, float | torch.Tensor]:
     """Single-rank first half: points (host or device) -> device, bounds, radius hint,
     Hilbert-sorted bucket tree. Everything is enqueued on the current stream; the one host
     sync is the over-full-cell check after the sort (see knn_engine.refine_heavy_cells),
     which waits for this stream only — so a caller can build the next point set on a side
-    stream while the current set's k-NN runs (bench.py --pipeline). `pre` = (box, curve
-    keys) of these device points computed already (SetStream LSKNN_PRE_KEYS)."""
+    stream while the current set's k-NN runs (bench.py --pipeline)."""
     info = info or RunInfo(PhaseTimer(False, comm.device))
     dev = comm.device
     n_local = points.shape[0]
-    if pre is not None:
-        box, keys = pre[0], (pre[1], None)
-    elif points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
+    if points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
         dpts, keys, box = upload_keyed(points, dev)
         points = dpts
     else:

@@ -35,7 +35,6 @@ from typing import Callable, Sequence
 import torch
 
 from ..models import knn_engine as E
-from ..ops import kernels as K
 from ..utils import trace
 from . import pipelines as PL
 from .comm import Comm
@@ -49,10 +48,6 @@ BUILD_AHEAD = os.environ.get("LSKNN_BUILD_AHEAD", "0") != "0"
 # beside it) is queued behind set i's index build, i.e. beside set i's k-NN, instead of
 # beside the build (env LSKNN_OUT_AFTER_BUILD; A/B in profiles/r4_final/README.md)
 OUT_AFTER_BUILD = os.environ.get("LSKNN_OUT_AFTER_BUILD", "0") == "1"
-# One rank: set i+1's bounds and curve keys (two short memory-bound passes) are computed on
-# the high-priority side stream beside set i's k-NN, once set i+1's upload has landed,
-# instead of at the head of set i+1's build beside set i's result copy (env LSKNN_PRE_KEYS)
-PRE_KEYS = os.environ.get("LSKNN_PRE_KEYS", "0") == "1"
 
 
 def _index_tensors(index: E.LocalIndex):
@@ -177,20 +172,15 @@ class SetStream:
         # right behind its k-NN, see knn_engine.query `deferred`) comes once set i+1's work
         # is queued; set i's output copy follows that check (a rerun rewrites the output)
         prev = None  # set i-1: see _query
-        pre: dict = {}  # set index -> (box, keys, event) computed beside the previous k-NN
         for i in range(n):
             self._uploaded(cur, i)  # set i's points are on the device
             pts = self._dbuf[i % 2]
             if i + 1 < n:
                 self._prefetch(i + 1, inputs[i + 1])
             info = new_info()
-            pk = pre.pop(i, None)
-            if pk is not None:
-                cur.wait_event(pk[2])
             with trace.range(f"lsknn:set {i}"):
                 info.timer.start()
-                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info,
-                                              pre=pk[:2] if pk is not None else None)
+                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info)
                 after = None
                 if OUT_AFTER_BUILD and prev is not None:
                     # set i-1's result copy beside set i's k-NN rather than its build
@@ -199,8 +189,6 @@ class SetStream:
                 rel = self._release(prev, outputs, after) if prev is not None else None
                 rec = self._query(i, index, hint2, info, outputs)
                 del index
-                if PRE_KEYS and i + 1 < n and self.gpu and not self.comm.distributed:
-                    pre[i + 1] = self._pre_keys(i + 1, cur)
             if rel is not None:  # set i-1's output, waited for once set i's k-NN is queued
                 rel[1].synchronize()
                 done(rel[0])
@@ -208,25 +196,6 @@ class SetStream:
             prev = rec
         if prev is not None:
             self._retire(prev, outputs, done)
-
-    def _pre_keys(self, j: int, cur):
-        """Set j's box and curve keys on the side stream once its upload has landed (the
-        upload event stays for the compute stream); -> (box, keys, event after them)."""
-        s2 = self.redist_stream
-        ev = self._copy_ev.get(j)
-        if ev is not None:
-            s2.wait_event(ev)
-        else:
-            s2.wait_stream(self.copy_stream)
-        nxt = self._dbuf[j % 2]
-        with torch.cuda.stream(s2):
-            box = PL.global_box(nxt, self.comm)
-            keys = K.morton(nxt, box, with_iota=False)[0]
-            done = torch.cuda.Event()
-            done.record(s2)
-        box.record_stream(cur)
-        keys.record_stream(cur)
-        return box, keys, done
 
     def _query(self, i, index, hint2, info, outputs):
         """Queue set i's k-NN (the kernel writes the pinned output itself when direct);

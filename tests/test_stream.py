@@ -98,25 +98,6 @@ def test_stream_single_gpu(direct, ahead):
     assert runner.last_info is not None
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("direct", [True, False])
-def test_stream_pre_keys_gpu(direct, monkeypatch):
-    """LSKNN_PRE_KEYS: set i+1's box and curve keys computed on the side stream beside set
-    i's k-NN (sets of different sizes: the device buffers are reallocated) — equal to the
-    CPU oracle."""
-    from mpi_cuda_largescaleknn_amd.parallel import stream as SM
-    monkeypatch.setattr(SM, "PRE_KEYS", True)
-    k = 16
-    cfg = E.KnnConfig(k=k)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    S = sets() + [GENERATORS["uniform"](30_000, seed=5)]
-    ins = [p.pin_memory() for p in S]
-    outs = [torch.full((p.shape[0],), -1.0).pin_memory() for p in S]
-    SetStream(SingleComm(dev), cfg, direct_out=direct).run(ins, outs)
-    for i, p in enumerate(S):
-        assert torch.equal(outs[i], oracle(p, k)), i
-
-
 @pytest.mark.parametrize("size", [1, 3])
 def test_compute_set_hook_redistributes_next_set_cpu(size):
     """The multi-rank two-phase API with the overlap hook (SetStream's GPU path): set B is
