@@ -72,6 +72,8 @@ FILE_FLAGS = {
     # iterative-ilp 0.138; same 72 VGPRs; profiles/archive/r2_kernel/README.txt)
     # candidates arrive in SGPRs: packed-math pairs would need them moved into VGPRs
     "knn_grid.hip": ["-fno-slp-vectorize"],
+    # the f16 fragment packing must stay in the explicit cvt_pkrtz / perm form
+    "knn_mfma.hip": ["-fno-slp-vectorize"],
     "knn_rows.hip": ["-fno-slp-vectorize", "-mllvm", "-disable-promote-alloca-to-vector",
                      "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
 }
