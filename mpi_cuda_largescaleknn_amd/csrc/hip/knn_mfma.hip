@@ -189,11 +189,13 @@ struct CellIter {
 };
 
 struct Stream {
-  // current cell (its masks) and the next one (slots in flight)
+  // current cell (its masks) and the next two (slots in flight: a cell change inside the
+  // tile builder waits for its slots, and with them for every older load)
   uint64_t need, free_;
-  uint32_t ca, ce, cxyz;  // per lane: slots of the current cell
-  uint32_t na, ne, nxyz;  // per lane: slots of the next cell (loaded ahead)
-  bool have_next;
+  uint32_t ca, ce, cxyz;     // per lane: slots of the current cell
+  uint32_t na, ne, nxyz;     // per lane: slots of the next cell
+  uint32_t ma, me, mxyz;     // per lane: slots of the cell after it
+  bool have_next, have_next2;
   uint32_t si, se;  // current segment (sorted-array range)
 };
 
@@ -274,9 +276,13 @@ __device__ __forceinline__ bool advance_cell(Wave &W, CellIter &I, Stream &S) {
     S.ca = S.na;
     S.ce = S.ne;
     S.cxyz = S.nxyz;
+    S.na = S.ma;
+    S.ne = S.me;
+    S.nxyz = S.mxyz;
+    S.have_next = S.have_next2;
     uint32_t cx, cy, cz;
-    S.have_next = next_cell(W, I, cx, cy, cz);
-    if (S.have_next) fetch_cell(W, cx, cy, cz, S.na, S.ne, S.nxyz);
+    S.have_next2 = S.have_next2 && next_cell(W, I, cx, cy, cz);
+    if (S.have_next2) fetch_cell(W, cx, cy, cz, S.ma, S.me, S.mxyz);
     cell_masks(W, S);
     if (S.need) return true;
   }
@@ -401,7 +407,10 @@ template <bool STRIDE>
 __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const lsk_knn_args A, const lsk_grid_view V) {
   // per wave: the band lists (32 queries x kStride dwords), then the current tile's points
   // (32 x float3: the append loop computes the exact d² of a band candidate from it)
-  __shared__ uint32_t lds[kWPB][kQ * kStride + 6 * kQ];
+#ifndef LSK_MF_LDSPAD
+#define LSK_MF_LDSPAD 0  // tuning: extra LDS dwords per wave (an occupancy probe)
+#endif
+  __shared__ uint32_t lds[kWPB][kQ * kStride + 6 * kQ + LSK_MF_LDSPAD];
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
   if (A.gate && *A.gate != A.gate_on) return;  // the device chose another kernel
@@ -545,6 +554,8 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
         uint32_t fx, fy, fz;
         S_.have_next = next_cell(W, I, fx, fy, fz);
         if (S_.have_next) fetch_cell(W, fx, fy, fz, S_.na, S_.ne, S_.nxyz);
+        S_.have_next2 = S_.have_next && next_cell(W, I, fx, fy, fz);
+        if (S_.have_next2) fetch_cell(W, fx, fy, fz, S_.ma, S_.me, S_.mxyz);
       }
       // Pipeline over PAIRS of tiles: the pair's points are in registers and the next
       // pair's loads are in flight. Both MFMAs are issued first; building the next pair
@@ -594,6 +605,8 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
         // the next pair: built and its loads issued under the MFMAs
         uint32_t ic = 0, id = 0;
         bool vc = false, vd = false;
+        // (both tiles are built before either's loads are issued: a cell change inside the
+        // builder waits for the slot loads, and with them for every older load)
         const bool hc = hb && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, ic, vc);
         const bool hd = hc && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, id, vd);
         float pcx = 0.f, pcy = 0.f, pcz = 0.f, pdx = 0.f, pdy = 0.f, pdz = 0.f;
