@@ -39,9 +39,18 @@ import sys
 import time
 
 # hardware queues per process: the HIP runtime reads this when torch loads it, so before
-# `import torch` (at least 8, see mpi_cuda_largescaleknn_amd/__init__.py)
-_hwq = max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4), int(os.environ.get("LSKNN_HW_QUEUES", "8")))
-os.environ["GPU_MAX_HW_QUEUES"] = str(min(_hwq, 32))
+# `import torch`. The benchmark's configuration raises it to at least LSKNN_HW_QUEUES
+# (default 8; the measured best, mpi_cuda_largescaleknn_amd/__init__.py) even over a lower
+# value in the environment (the GPU box exports HIP's default, 4); the JSON records it.
+def _int_env(name: str, default: int) -> int:
+    try:
+        return int(os.environ.get(name, "") or default)
+    except ValueError:
+        return default
+
+
+HW_QUEUES = min(max(_int_env("GPU_MAX_HW_QUEUES", 4), _int_env("LSKNN_HW_QUEUES", 8)), 32)
+os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 import torch  # noqa: E402
 
@@ -74,6 +83,26 @@ def metric_name(n_total: int, k: int) -> str:
     pts = f"{n_total / 1e9:g}B" if n_total >= 10**9 else f"{n_total / 1e6:g}M"
     return f"Mpoints/sec kNN-distance (k={k}) on {pts} float3 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no numbers
+BENCH_TIMEOUT_S = 150  # progress timeout of every rank (LSKNN_TIMEOUT overrides)
+
+
+def comm_info(comm) -> dict:
+    """Which communicator moved the data and which RCCL library it runs."""
+    inner = getattr(comm, "inner", comm)
+    backend = getattr(inner, "backend", "single") if comm.distributed else "single"
+    out = {"backend": backend, "rccl_version": None}
+    if backend == "rccl":
+        v = int(getattr(inner, "version", 0) or 0)  # NCCL_VERSION_CODE: major*10000+minor*100+patch
+        out["rccl_version"] = f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v else None
+        out["rccl_library"] = "ROCm librccl (native communicator, parallel/rccl.py)"
+    elif backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            out["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001 - reporting only
+            pass
+        out["rccl_library"] = "torch.distributed ProcessGroupNCCL (torch's bundled librccl)"
+    return out
 
 
 def parse():
@@ -175,10 +204,12 @@ def main():
     if rc is not None:
         sys.exit(rc)
     # a hung collective ends the job (watchdog + collective timeout) long before the
-    # driver's limit; one rank per GPU (ranks beyond the device count wrap: rehearsals
-    # with LSKNN_DIST_BACKEND=gloo only, RCCL refuses two ranks on one GPU); pinned
-    # buffers on the GPU's NUMA node
-    os.environ.setdefault("LSKNN_TIMEOUT", "600")
+    # driver's 600 s limit, and the watchdog names the rank and the collective it stalled
+    # in ("#r/P: watchdog: timeout in alltoallv: ...") inside the tail the driver keeps; one
+    # rank per GPU (ranks beyond the device count wrap: rehearsals with
+    # LSKNN_DIST_BACKEND=gloo only, RCCL refuses two ranks on one GPU); pinned buffers on
+    # the GPU's NUMA node
+    os.environ.setdefault("LSKNN_TIMEOUT", str(BENCH_TIMEOUT_S))
     launch = LA.init(device_pref=args.device, force_distributed=args.force_dist or None,
                      verbose=args.phases)
     world, rank, device, comm = launch.size, launch.rank, launch.device, launch.comm
@@ -208,6 +239,7 @@ def main():
     host_pts, host_out = host_sets[0], host_outs[0]
 
     info_last = None
+    graph_kernels: list = []
     # one GPU rank: the pinned output is passed down and pipelines.query_into picks direct
     # PCIe writes or device buffer + copy (--direct-out forces one)
     single_gpu = not comm.distributed and device.type == "cuda"
@@ -267,9 +299,13 @@ def main():
         E.REFINE_CAPTURE = E.LAST_REFINED
         E.prepare_capture(device)  # failure-word peaks over every replay
         graph = torch.cuda.CUDAGraph()
+        E.reset_kernels_used()
         with torch.cuda.graph(graph):
             _step()
         _sync(device)
+        # the replays run exactly the captured launches: report the capture's kernels
+        # (the reset before the timed steps would otherwise leave the list empty)
+        graph_kernels = E.kernels_used()
 
         def step():  # noqa: F811 — graph replay replaces the eager step
             with trace.range("lsknn:step"):
@@ -317,6 +353,8 @@ def main():
     comm.allreduce_(t, "max")
     elapsed = float(t.item())
     kernels_timed = E.kernels_used()  # (gate reads: after the clock)
+    if graph is not None:
+        kernels_timed = sorted(set(kernels_timed) | set(graph_kernels))
 
     ms = elapsed / args.steps * 1e3
     value = n_total * args.steps / elapsed / 1e6
@@ -392,11 +430,12 @@ def main():
                                 f"spatial-redistribute+halo x{world}" if args.variant == "unordered"
                                 else f"halo x{world}"),
                 "k": args.k,
-                "comm": (getattr(getattr(comm, "inner", comm), "backend", "single")
-                         if comm.distributed else "single"),
+                "comm": comm_info(comm)["backend"],
+                "comm_info": comm_info(comm),
                 "ranks": world,
                 "collectives_per_step": round(coll_per_step, 2),
                 "hip_graph": graph is not None,
+                "hw_queues": HW_QUEUES,
                 "pipelined": pipelined,
                 "heavy_cells_unrefined": heavy_unrefined,
                 "knn_kernels": kernels_timed,

@@ -158,8 +158,9 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     if box is None:
         box = K.bounds(points)
     gpu = K.is_gpu(points)
-    if keys is not None:
-        skeys, perm = K.sort_pairs(keys[0], keys[1], 30)
+    if keys is not None:  # (keys, None): values 0..n-1 generated by the sort
+        skeys, perm = (K.sort_pairs(keys[0], keys[1], 30) if keys[1] is not None
+                       else K.sort_keys_iota(keys[0], 30))
     elif gpu:  # (the sort's first pass generates the values: no iota array)
         skeys, perm = K.sort_keys_iota(K.morton(points, box, with_iota=False)[0], 30)
     else:

@@ -211,7 +211,7 @@ class Watchdog:
                         self.store.set(ABORT_KEY, f"rank {self.rank} timed out in {HEARTBEAT.what}")
                     except Exception:  # noqa: BLE001
                         pass
-                self._die(f"watchdog: no progress for {idle:.0f}s (last: {HEARTBEAT.what}), aborting",
+                self._die(f"watchdog: timeout in {HEARTBEAT.what}: no progress for {idle:.0f}s, aborting",
                           EXIT_TIMEOUT)
 
 

@@ -549,8 +549,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
             pre = torch.cuda.Event()
             pre.record(torch.cuda.current_stream(index.device))
         d2 = E.query(index, cfg, hint2, stats=stats, final_out=final_out, keep_d2=True,
-                     deferred=None if capturing or not gpu else pend,
-                     chunks=KNN_CHUNKS if hook is not None else 1)
+                     deferred=None if capturing or not gpu else pend)
         if hook is not None:
             # the hook's work follows what precedes the k-NN (REDIST_UNDER_KNN), else the k-NN
             st = hook(pre if pre is not None else (torch.cuda.current_stream(index.device) if gpu else None))
@@ -607,7 +606,7 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         if not gpu:
             recv = _halo_send(index, radii, comm, cfg, info, marks=False)
         E.query(index, cfg, hint2, stats=stats, final_out=final_out, out=d2, groups=ilist, ngroups=ng,
-                ngroups_dev=icnt, deferred=pend if gpu else None, chunks=KNN_CHUNKS if gpu else 1)
+                ngroups_dev=icnt, deferred=pend if gpu else None)
         if gpu:
             ev_int = torch.cuda.Event()
             ev_int.record(comp)
@@ -629,6 +628,10 @@ def knn_with_halo(index: E.LocalIndex, comm: Comm, cfg: E.KnnConfig, hint2: floa
         cur.wait_stream(side)
         recv.record_stream(cur)
         d2.record_stream(cur)
+        # (the group lists: a failure-list overflow reruns the exact kernel on `cur` inside
+        # E.settle, reading them)
+        for t in (blist, ilist, bcnt, icnt):
+            t.record_stream(cur)
         final_out.record_stream(comp)
         radii.record_stream(side)
         E.settle(pend)
@@ -669,11 +672,9 @@ def _check_out(out: torch.Tensor | None, n: int, points: torch.Tensor) -> torch.
 
 
 
-# Passes with work of other streams to run beside them (the next set's redistribution,
-# the halo exchange) go out as this many launches: a running k-NN grid holds every CU slot
-# until its last workgroup is dispatched, so a high-priority stream's kernels only start
-# at a kernel boundary (env LSKNN_KNN_CHUNKS; 1 = one launch).
-KNN_CHUNKS = int(os.environ.get("LSKNN_KNN_CHUNKS", "1"))
+# (Splitting a pass into several launches so that high-priority streams' kernels get CU
+# slots at the kernel boundaries was measured and dropped: no change at 1e8 with 8
+# hardware queues, profiles/r4_s1/fd_c4, fd_c8.)
 # The next set's redistribution (SetStream's hook) is ordered after what precedes the local
 # k-NN launch, so it runs beside the k-NN once its upload has landed (forced 1-rank RCCL
 # 1e8 stream with 8 hardware queues: 997.4 vs 980.5 Mpts/s ordered after the k-NN;
@@ -755,16 +756,19 @@ def upload_keyed(host_pts: torch.Tensor, dev: torch.device, chunk: int | None = 
 
 
 def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
-                info: RunInfo | None = None) -> tuple[E.LocalIndex, float | torch.Tensor]:
+                info: RunInfo | None = None, pre: tuple | None = None) -> tuple[E.LocalIndex, float | torch.Tensor]:
     """Single-rank first half: points (host or device) -> device, bounds, radius hint,
     Hilbert-sorted bucket tree. Everything is enqueued on the current stream; the one host
     sync is the over-full-cell check after the sort (see knn_engine.refine_heavy_cells),
     which waits for this stream only — so a caller can build the next point set on a side
-    stream while the current set's k-NN runs (bench.py --pipeline)."""
+    stream while the current set's k-NN runs (bench.py --pipeline). `pre` = (box, curve
+    keys) of these device points computed already (SetStream PRE_KEYS)."""
     info = info or RunInfo(PhaseTimer(False, comm.device))
     dev = comm.device
     n_local = points.shape[0]
-    if points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
+    if pre is not None:
+        box, keys = pre[0], (pre[1], None)
+    elif points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
         dpts, keys, box = upload_keyed(points, dev)
         points = dpts
     else:
@@ -879,8 +883,6 @@ class Redistributed:
     recv_counts: list
     send_perm: torch.Tensor      # local input row of each sent row
     send_counts: list
-    index: E.LocalIndex | None = None  # built ahead (SetStream), else by compute_set
-    index_ready: object = None         # event after which `index` is complete
     n_total: int | None = None         # points of the whole set (grid level of the global box)
 
 
@@ -901,36 +903,15 @@ def redistribute_set(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total
                          n_total=n_total)
 
 
-def build_ahead(P: Redistributed, stream, users) -> None:
-    """Build P's index on `stream` (after the work queued there so far) and mark it ready
-    with an event; its tensors are kept for the streams in `users` (record_stream)."""
-    with torch.cuda.stream(stream):
-        index = E.build_index(P.owned, P.box, grid=True, density_n=P.n_total)
-    P.owned.record_stream(stream)
-    for t in (index.pts, index.perm, index.nodes, index.qnodes, index.box) + \
-            ((index.grid.slots,) if index.grid is not None else ()):
-        for u in users:
-            t.record_stream(u)
-    ev = torch.cuda.Event()
-    ev.record(stream)
-    P.index, P.index_ready = index, ev
-
-
 def compute_set(P: Redistributed, comm: Comm, cfg: E.KnnConfig, info: RunInfo | None = None,
                 out: torch.Tensor | None = None, hook=None) -> torch.Tensor:
-    """Second half: bucket tree of the owned points (or P.index built ahead), local k-NN +
-    halo exchange + re-query,
+    """Second half: bucket tree of the owned points, local k-NN + halo exchange + re-query,
     distances back to their origin ranks in input order (into `out` if given). `hook`:
     see knn_with_halo; it returns the stream its collectives ran on, and the result
     return is ordered after it (one communicator: no concurrent collectives)."""
     info = info or RunInfo(PhaseTimer(False, comm.device))
     dev = comm.device
-    if P.index is not None:
-        index = P.index
-        if P.index_ready is not None:
-            torch.cuda.current_stream(dev).wait_event(P.index_ready)
-    else:
-        index = E.build_index(P.owned, P.box, grid=True, density_n=P.n_total)
+    index = E.build_index(P.owned, P.box, grid=True, density_n=P.n_total)
     info.timer.mark("build")
     dist_owned = torch.empty(index.n, dtype=torch.float32, device=dev)
     used: list = []

@@ -35,19 +35,22 @@ from typing import Callable, Sequence
 import torch
 
 from ..models import knn_engine as E
+from ..ops import kernels as K
 from ..utils import trace
 from . import pipelines as PL
 from .comm import Comm
 
 
-# one rank: set i+1's index is built on the high-priority side stream under set i's k-NN
-# (measured slower: 1B k=100 1168 vs 1106 ms per set; the build's workgroups hold CU slots
-# among the k-NN's far longer than the build takes alone — kept as an option)
-BUILD_AHEAD = os.environ.get("LSKNN_BUILD_AHEAD", "0") != "0"
-# One rank: set i-1's result copy to host (device->host PCIe traffic slows whatever runs
-# beside it) is queued behind set i's index build, i.e. beside set i's k-NN, instead of
-# beside the build (env LSKNN_OUT_AFTER_BUILD; A/B in profiles/r4_final/README.md)
-OUT_AFTER_BUILD = os.environ.get("LSKNN_OUT_AFTER_BUILD", "0") == "1"
+# Measured and dropped (rounds 3-4; the A/Bs stay in profiles/): building set i+1's index
+# on a side stream under set i's k-NN (1B k=100: 1168 vs 1106 ms per set — the build's
+# workgroups hold CU slots among the k-NN's far longer than the build takes alone), and
+# queueing set i-1's result copy behind set i's build instead of beside it
+# (profiles/r4_final/README.md).
+# One rank: set i+1's bounds and curve keys (two short memory-bound passes) are computed on
+# the high-priority side stream beside set i's k-NN, once set i+1's upload has landed,
+# instead of at the head of set i+1's build beside set i-1's result copy (env
+# LSKNN_PRE_KEYS; 1 = on).
+PRE_KEYS = os.environ.get("LSKNN_PRE_KEYS", "1") == "1"
 
 
 def _index_tensors(index: E.LocalIndex):
@@ -69,7 +72,7 @@ class SetStream:
     """
 
     def __init__(self, comm: Comm, cfg: E.KnnConfig, direct_out: bool = True,
-                 build_ahead: bool | None = None, variant: str = "unordered"):
+                 variant: str = "unordered", pre_keys: bool | None = None):
         if variant not in ("unordered", "prepartitioned"):
             raise ValueError(f"SetStream: variant must be unordered or prepartitioned, not {variant!r}")
         self.comm = comm
@@ -78,9 +81,7 @@ class SetStream:
         self.device = comm.device
         self.gpu = self.device.type == "cuda"
         self.direct_out = bool(direct_out) and not comm.distributed
-        if build_ahead is None:
-            build_ahead = BUILD_AHEAD
-        self.build_ahead = bool(build_ahead)
+        self.pre_keys = PRE_KEYS if pre_keys is None else bool(pre_keys)
         if self.gpu:
             self.copy_stream = torch.cuda.Stream(self.device)
             self.out_stream = torch.cuda.Stream(self.device)
@@ -149,8 +150,6 @@ class SetStream:
                     return self._run_prepartitioned(inputs, outputs, new_info, done)
                 if self.comm.distributed:
                     return self._run_distributed(inputs, outputs, n_totals, new_info, done)
-                if self.build_ahead:  # (one rank)
-                    return self._run_build_ahead(inputs, outputs, n_totals, new_info, done)
                 return self._run_local(inputs, outputs, n_totals, new_info, done)
         for i in range(n):  # CPU: one set after the other
             info = new_info()
@@ -172,23 +171,25 @@ class SetStream:
         # right behind its k-NN, see knn_engine.query `deferred`) comes once set i+1's work
         # is queued; set i's output copy follows that check (a rerun rewrites the output)
         prev = None  # set i-1: see _query
+        pre: dict = {}  # set index -> (box, keys, event) computed beside the previous k-NN
         for i in range(n):
             self._uploaded(cur, i)  # set i's points are on the device
             pts = self._dbuf[i % 2]
             if i + 1 < n:
                 self._prefetch(i + 1, inputs[i + 1])
             info = new_info()
+            pk = pre.pop(i, None)
+            if pk is not None:
+                cur.wait_event(pk[2])
             with trace.range(f"lsknn:set {i}"):
                 info.timer.start()
-                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info)
-                after = None
-                if OUT_AFTER_BUILD and prev is not None:
-                    # set i-1's result copy beside set i's k-NN rather than its build
-                    after = torch.cuda.Event()
-                    after.record(cur)
-                rel = self._release(prev, outputs, after) if prev is not None else None
+                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[i] or pts.shape[0], info,
+                                              pre=pk[:2] if pk is not None else None)
+                rel = self._release(prev, outputs) if prev is not None else None
                 rec = self._query(i, index, hint2, info, outputs)
                 del index
+                if self.pre_keys and i + 1 < n:
+                    pre[i + 1] = self._pre_keys(i + 1, cur)
             if rel is not None:  # set i-1's output, waited for once set i's k-NN is queued
                 rel[1].synchronize()
                 done(rel[0])
@@ -235,66 +236,24 @@ class SetStream:
             res.record_stream(self.out_stream)
         return j, ev
 
-    def _run_build_ahead(self, inputs, outputs, n_totals, new_info, done) -> None:
-        """One rank, index builds off the compute stream: set i+1's bounds, sort, tree and
-        grid are queued on the high-priority side stream right after set i's k-NN launch.
-        The k-NN grid is VALU-bound and the build kernels memory-bound; the build's
-        workgroups take CU slots as the k-NN's retire, so the compute stream runs k-NN after
-        k-NN with no build between them. The index tensors are allocated on the side stream
-        and read on the compute stream (record_stream keeps them until that read is done).
-        Sets alive at once: the one being retired, the one in the k-NN, the one being built
-        and the one being uploaded after the retired one is released."""
-        n = len(inputs)
-        dev = self.device
-        cur = torch.cuda.current_stream(dev)
-        side = self.redist_stream
-        if n == 0:
-            return
-
-        def build(j: int):
-            # set j's points are on the device (copy stream), then its index on `side`
-            self._uploaded(side, j)
-            info = new_info()
-            info.timer.start()
-            with torch.cuda.stream(side):
-                pts = self._dbuf[j % 2]
-                index, hint2 = PL.local_build(pts, self.comm, self.cfg, n_totals[j] or pts.shape[0], info)
-            for t in _index_tensors(index):
-                t.record_stream(cur)
-            if isinstance(hint2, torch.Tensor):
-                hint2.record_stream(cur)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            return index, hint2, info, ev
-
-        self._prefetch(0, inputs[0])
-        nxt = build(0)
-        if n > 1:
-            self._prefetch_after(1, inputs[1], None)
-        prev = None
-        for i in range(n):
-            index, hint2, info, bev = nxt
-            cur.wait_event(bev)
-            with trace.range(f"lsknn:set {i}"):
-                rec = self._query(i, index, hint2, info, outputs)
-            del index
-            if i + 1 < n:
-                nxt = build(i + 1)  # under set i's k-NN
-            if prev is not None:
-                # set i-1's failure word (its k-NN ran before set i's; a rerun goes behind
-                # set i's k-NN with set i-1's index still alive), output, release
-                self._retire(prev, outputs, done)
-            if i + 2 < n:
-                # set i+2 reuses set i's input buffer: free once set i's build is done
-                self._prefetch_after(i + 2, inputs[i + 2], bev)
-            self.last_info = info
-            prev = rec
-        self._retire(prev, outputs, done)
-
-    def _build_stream(self):
-        if getattr(self, "_bst", None) is None:
-            self._bst = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
-        return self._bst
+    def _pre_keys(self, j: int, cur):
+        """Set j's box and curve keys on the side stream once its upload has landed (the
+        upload event stays for the compute stream); -> (box, keys, event after them)."""
+        s2 = self.redist_stream
+        ev = self._copy_ev.get(j)
+        if ev is not None:
+            s2.wait_event(ev)
+        else:
+            s2.wait_stream(self.copy_stream)
+        nxt = self._dbuf[j % 2]
+        with torch.cuda.stream(s2):
+            box = PL.global_box(nxt, self.comm)
+            keys = K.morton(nxt, box, with_iota=False)[0]
+            done = torch.cuda.Event()
+            done.record(s2)
+        box.record_stream(cur)
+        keys.record_stream(cur)
+        return box, keys, done
 
     def _prefetch_after(self, j: int, host: torch.Tensor, ev) -> None:
         # copy set j into its buffer once `ev` (the build that last read it) is done
@@ -357,7 +316,6 @@ class SetStream:
         comm, cfg, dev = self.comm, self.cfg, self.device
         cur = torch.cuda.current_stream(dev)
         redist = self.redist_stream
-        bst = self._build_stream()
         n = len(inputs)
         for j in range(n):  # global point counts (one small all-reduce per unknown set)
             if n_totals[j] is None:
@@ -409,11 +367,6 @@ class SetStream:
                     e = torch.cuda.Event()
                     e.record(redist)
                 red_ev[j % 2] = e
-                if self.build_ahead:
-                    # and its index, on a stream of its own (the collectives' stream, which
-                    # set i's halo exchange and result return wait for, stays short)
-                    bst.wait_stream(redist)
-                    PL.build_ahead(nxt["P"], bst, [cur])
                 return redist
 
             with trace.range(f"lsknn:set {i}"):

@@ -59,6 +59,9 @@ def test_bench_single_gpu_graph_and_eager(graph):
     assert rec["config"]["all_finite"] is True
     assert rec["config"]["hip_graph"] is (graph == "1")
     assert rec["config"]["sampled_exact"] == "256/256"
+    # the kernels that ran are reported in graph mode too (captured launches)
+    assert rec["config"]["knn_kernels"], rec["config"]
+    assert rec["config"]["hw_queues"] >= 8
 
 
 @pytest.mark.gpu
@@ -78,15 +81,13 @@ def test_bench_single_gpu_pipelined():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ahead", ["1", "0"])
-def test_bench_pipelined_forced_rccl_single_gpu(ahead):
+def test_bench_pipelined_forced_rccl_single_gpu():
     """--pipeline 1 on the multi-rank path (1-rank RCCL group): device-resident input per
-    step, plain (non-streamed) redistribution, the next set's index built ahead on a side
-    stream (or by compute_set), both sets exact."""
+    step, plain (non-streamed) redistribution beside the previous set's k-NN, both sets
+    exact."""
     out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
                           "--force-dist", "--pipeline", "1"],
-                         cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
-                                            LSKNN_BUILD_AHEAD=ahead),
+                         cwd=ROOT, env=dict(_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port())),
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = _json_line(out.stdout)
@@ -111,6 +112,9 @@ def test_bench_forced_rccl_single_gpu(backend):
     assert rec["config"]["sampled_exact"] == "256/256"
     assert "alltoallv_points" in rec["detail"]["phase_ms_max_over_ranks"]
     assert rec["config"]["comm"] == backend
+    # which RCCL library moved the data: torch's bundled one or ROCm's (native communicator)
+    v = rec["config"]["comm_info"]["rccl_version"]
+    assert v and v.split(".")[0] == "2", rec["config"]["comm_info"]
 
 
 @pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])
@@ -192,6 +196,7 @@ def test_bench_self_launches_gpus_ranks_on_cpu():
     rec = _json_line(out.stdout)
     assert rec["n_gpus"] == 4 and rec["config"]["ranks"] == 4
     assert rec["config"]["comm"] == "gloo"
+    assert rec["config"]["comm_info"]["backend"] == "gloo"
     assert rec["config"]["sampled_exact"] == "256/256"
     assert rec["config"]["collectives_per_step"] > 0
     assert len(rec["detail"]["owned_points_per_rank"]) == 4
@@ -243,11 +248,12 @@ def test_ref_memory_arithmetic():
         RA.check_ref_fits(1_000_000_000, 100, 288 * 10**9, 1)
 
 
-@pytest.mark.parametrize("env,want", [(None, "8"), ("4", "8"), ("16", "16"), ("64", "32")])
-def test_hardware_queue_floor(env, want):
-    """Importing the package (bench.py does the same before `import torch`) raises the HIP
-    hardware-queue count to at least 8 — the box's 4 made unrelated streams share in-order
-    queues — keeps a larger setting and never exceeds 32."""
+@pytest.mark.parametrize("env,want", [(None, "8"), ("4", "4"), ("16", "16"), ("abc", "abc")])
+def test_hardware_queue_default(env, want):
+    """Importing the package fills in the HIP hardware-queue count (8: the box's default 4
+    made unrelated streams share in-order queues) only when it is unset: an explicit value
+    is kept (a lower one with a notice), a malformed one does not break the import
+    (ADVICE r4)."""
     e = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "LSKNN_HW_QUEUES")}
     if env is not None:
         e["GPU_MAX_HW_QUEUES"] = env
@@ -255,3 +261,17 @@ def test_hardware_queue_floor(env, want):
                           "print(os.environ['GPU_MAX_HW_QUEUES'])"], cwd=ROOT, env=e,
                          capture_output=True, text=True, check=True)
     assert out.stdout.strip() == want
+    assert ("kept" in out.stderr) == (env == "4")
+
+
+@pytest.mark.parametrize("env,want", [(None, 8), ("4", 8), ("16", 16), ("64", 32), ("abc", 8)])
+def test_bench_hardware_queue_floor(env, want):
+    """bench.py's own configuration: at least 8 queues (the measured best) even over the
+    box's exported 4, at most 32, recorded in the JSON (config.hw_queues)."""
+    e = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "LSKNN_HW_QUEUES")}
+    if env is not None:
+        e["GPU_MAX_HW_QUEUES"] = env
+    out = subprocess.run([sys.executable, "-c", "import os, bench; print(bench.HW_QUEUES, "
+                          "os.environ['GPU_MAX_HW_QUEUES'])"], cwd=ROOT, env=e,
+                         capture_output=True, text=True, check=True)
+    assert out.stdout.split() == [str(want), str(want)]

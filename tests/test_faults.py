@@ -115,3 +115,25 @@ def test_watchdog_aborts_on_communicator_error(tmp_path):
     assert out.returncode == 5, (out.returncode, out.stderr)
     assert "remote process exited" in out.stderr
     assert flag.exists()
+
+
+def test_bench_hang_names_the_collective():
+    """bench.py's own progress timeout (bench.BENCH_TIMEOUT_S = 150 s, well under the
+    driver's 600 s; shortened here through LSKNN_TIMEOUT): a rank hung in a collective
+    ends the self-launched job non-zero, and the kept tail names the rank and the op."""
+    import bench
+
+    assert bench.BENCH_TIMEOUT_S <= 200
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2",
+               LSKNN_FAULT="rank=1,op=alltoallv,kind=hang", LSKNN_TIMEOUT="8")
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    t = time.monotonic()
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--points", "2e4", "--k", "8",
+                        "--steps", "1", "--warmup", "0", "--verify", "0"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    dt = time.monotonic() - t
+    assert p.returncode != 0
+    assert "#1/2: injected fault (hang) in alltoallv" in p.stderr
+    assert "timeout in alltoallv" in p.stderr or "timed out in alltoallv" in p.stderr, p.stderr[-2000:]
+    assert dt < 150

@@ -79,19 +79,19 @@ def test_stream_length_mismatch():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("direct", [True, False])
-@pytest.mark.parametrize("ahead", [True, False])
-def test_stream_single_gpu(direct, ahead):
-    """One rank on the GPU: pinned host sets of different sizes, the kernel writing the
-    pinned outputs directly (or device results copied back), the next set's index built
-    on the side stream under the current k-NN (or on the compute stream between them),
-    equal to the CPU oracle."""
+@pytest.mark.parametrize("pre", [True, False])
+def test_stream_single_gpu(direct, pre):
+    """One rank on the GPU: pinned host sets of different sizes (the device buffers are
+    reallocated), the kernel writing the pinned outputs directly (or device results copied
+    back), the next set's box and curve keys computed on the side stream beside the
+    current k-NN (PRE_KEYS) or at the head of its build, equal to the CPU oracle."""
     k = 16
     cfg = E.KnnConfig(k=k)
     dev = torch.device("cuda", torch.cuda.current_device())
     S = sets() + [GENERATORS["uniform"](30_000, seed=5)]
     ins = [p.pin_memory() for p in S]
     outs = [torch.full((p.shape[0],), -1.0).pin_memory() for p in S]
-    runner = SetStream(SingleComm(dev), cfg, direct_out=direct, build_ahead=ahead)
+    runner = SetStream(SingleComm(dev), cfg, direct_out=direct, pre_keys=pre)
     runner.run(ins, outs)
     for i, p in enumerate(S):
         assert torch.equal(outs[i], oracle(p, k)), i
@@ -188,7 +188,7 @@ def test_stream_failure_overflow_rerun_gpu(ahead, monkeypatch):
     """every k-NN launch hands every 7th query to the backstop and the failure
     list holds only 16, so every set's failure word overflows and the host reruns the
     whole set on the exact kernel while the next set is already queued — set i's output
-    copy must follow that rerun (SetStream._release), in the default and the build-ahead
+    copy must follow that rerun (SetStream._release), with and without the pre-computed keys (PRE_KEYS)
     modes, with lazy inputs / outputs released in on_done."""
     from mpi_cuda_largescaleknn_amd.ops import kernels as KK
 
@@ -207,7 +207,7 @@ def test_stream_failure_overflow_rerun_gpu(ahead, monkeypatch):
         ins.alive.pop(i)
         outs.alive.pop(i)
 
-    SetStream(SingleComm(dev), E.KnnConfig(k=k), direct_out=False, build_ahead=ahead).run(ins, outs, on_done=on_done)
+    SetStream(SingleComm(dev), E.KnnConfig(k=k), direct_out=False, pre_keys=ahead).run(ins, outs, on_done=on_done)
     assert done == list(range(len(S)))
 
 
