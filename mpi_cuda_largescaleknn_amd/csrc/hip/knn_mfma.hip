@@ -149,6 +149,21 @@ __device__ __forceinline__ f16x8 as_frag(uint32_t d0, uint32_t d1, uint32_t d2, 
 }
 constexpr uint32_t kOnes16 = 0x3C003C00u;  // (1.0, 1.0) in f16
 
+// Point loads the compiler does not see as loads: issued unconditionally (it cannot sink a
+// load into the one path that uses it, which would leave other paths with fewer younger
+// loads and force vmcnt(0)), waited for by hand with a count that holds on every path.
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ f32x3 ld_point(const float *pts, uint32_t i) {
+  f32x3 v;
+  asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(v) : "v"(pts + 3ull * i) : "memory");
+  return v;
+}
+// all but the two youngest vector-memory operations done; the operands are the registers
+// the wait makes valid (no use of them can move above it)
+__device__ __forceinline__ void wait_vm2(f32x3 &a, f32x3 &b) {
+  asm volatile("s_waitcnt vmcnt(2)" : "+v"(a), "+v"(b) : : "memory");
+}
+
 // A fragment of candidate (px, py, pz) (centred, scaled) for this lane's half h of K:
 // h = 0: [xh xl xh xl yh yl yh yl]; h = 1: [zh zl zh zl pph ppl 1 1] (pp = |p|²).
 __device__ __forceinline__ f16x8 frag_a(float px, float py, float pz, bool upper) {
@@ -403,14 +418,28 @@ __device__ __forceinline__ void net32_select(uint32_t *v, uint32_t m, uint32_t &
   out = r;
 }
 
+#ifndef LSK_MF_GBAND
+#define LSK_MF_GBAND 0  // tuning: band lists in global memory (an occupancy probe: no LDS limit)
+#endif
+#if LSK_MF_GBAND
+#define BAND(jj, e) gband[(size_t)(e) * kQ + (jj)]
+#else
+#define BAND(jj, e) region[(jj) * kStride + (e)]
+#endif
+
 template <bool STRIDE>
-__global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const lsk_knn_args A, const lsk_grid_view V) {
+__global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const lsk_knn_args A, const lsk_grid_view V,
+                                                                         uint32_t *gband_all) {
   // per wave: the band lists (32 queries x kStride dwords), then the current tile's points
   // (32 x float3: the append loop computes the exact d² of a band candidate from it)
 #ifndef LSK_MF_LDSPAD
 #define LSK_MF_LDSPAD 0  // tuning: extra LDS dwords per wave (an occupancy probe)
 #endif
+#if LSK_MF_GBAND
+  __shared__ uint32_t lds[kWPB][6 * kQ + LSK_MF_LDSPAD];
+#else
   __shared__ uint32_t lds[kWPB][kQ * kStride + 6 * kQ + LSK_MF_LDSPAD];
+#endif
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
   if (A.gate && *A.gate != A.gate_on) return;  // the device chose another kernel
@@ -420,8 +449,26 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
   if (A.wave_end > 0) gend = min(gend, (uint64_t)A.wave_end);
   uint64_t g = STRIDE ? (uint64_t)blockIdx.x + (uint32_t)A.wave_base
                       : (uint64_t)lsk::xcd_remap(blockIdx.x, gridDim.x) + (uint32_t)A.wave_base;
+  uint64_t gstep = gridDim.x;
+#if LSK_MF_GBAND
+  // persistent blocks, XCD-aware: the blocks of XCD x (blockIdx % 8, the dispatch order)
+  // walk the x-th eighth of the groups
+  if (STRIDE && (gridDim.x & 7u) == 0u) {
+    const uint64_t nall = gend - (uint64_t)(uint32_t)A.wave_base, x = blockIdx.x & 7u;
+    const uint64_t lo = (uint32_t)A.wave_base + nall * x / 8u, hi = (uint32_t)A.wave_base + nall * (x + 1u) / 8u;
+    g = lo + (blockIdx.x >> 3);
+    gend = hi;
+    gstep = gridDim.x >> 3;
+  }
+#endif
+#if LSK_MF_GBAND
+  uint32_t *gband = gband_all + ((size_t)blockIdx.x * kWPB + (size_t)wid) * kQ * kCapQ;
+  float *stage = (float *)lds[wid];
+#else
+  (void)gband_all;
   uint32_t *region = lds[wid];
   float *stage = (float *)(lds[wid] + kQ * kStride);
+#endif
   const bool upper = lane >= 32;
   const uint32_t j = (uint32_t)lane & 31u;
   const uint32_t k = (uint32_t)A.k;
@@ -454,7 +501,7 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
   const float cut2 = (A.cut2 == A.cut2) ? fmaxf(A.cut2, 0.f) : __builtin_inff();
   const uint32_t cut_b = fbits(cut2);
 
-  for (; g < gend; g += STRIDE ? (uint64_t)gridDim.x : gend) {
+  for (; g < gend; g += STRIDE ? gstep : gend) {
     const uint32_t grp = lsk::uniform(A.groups ? A.groups[g] : (uint32_t)g);
     const int64_t q0 = (int64_t)grp * lsk::kBucket + (int64_t)wid * kQ;
     const int64_t qi = q0 + (int64_t)j;
@@ -557,33 +604,41 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
         S_.have_next2 = S_.have_next && next_cell(W, I, fx, fy, fz);
         if (S_.have_next2) fetch_cell(W, fx, fy, fz, S_.ma, S_.me, S_.mxyz);
       }
-      // Pipeline over PAIRS of tiles: the pair's points are in registers and the next
-      // pair's loads are in flight. Both MFMAs are issued first; building the next pair
-      // covers their latency. Band candidates of the pair get their exact canonical d² in
-      // one append loop over a 32-bit mask (the pair's points staged in LDS): below L ->
-      // counted, in [L, H) -> the band list holds the exact bits.
+      // Pipeline over PAIRS of tiles, two pairs in flight: pair X is processed while pair
+      // Y's loads are outstanding, and X's registers take the pair after Y (loads issued
+      // under X's MFMAs, consumed two half-steps later). The loop is unrolled by two (X, Y)
+      // so no loaded register is copied (a copy would wait for its load), and every point
+      // load is issued unconditionally (a clamped index when there is no tile): with equal
+      // load counts on every path the waits for a pair are vmcnt(2), not vmcnt(0). Band
+      // candidates of the pair get their exact canonical d² in one append loop over a
+      // 32-bit mask (the pair's points staged in LDS): below L -> counted, in [L, H) -> the
+      // band list holds the exact bits.
       const uint32_t Lb = fbits(L), Hb = fbits(H);
       uint32_t o1, o2, o3, b0, b1, b2, b3;
-      uint32_t ia = 0, ib = 0;
-      bool va = false, vb = false;
-      bool ha = next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, ia, va);
-      bool hb = ha && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, ib, vb);
-      float pax = 0.f, pay = 0.f, paz = 0.f, pbx = 0.f, pby = 0.f, pbz = 0.f;
-      if (ha) {
-        pax = W.G.pts[3ull * ia];
-        pay = W.G.pts[3ull * ia + 1];
-        paz = W.G.pts[3ull * ia + 2];
-      }
-      if (hb) {
-        pbx = W.G.pts[3ull * ib];
-        pby = W.G.pts[3ull * ib + 1];
-        pbz = W.G.pts[3ull * ib + 2];
-      }
       const uint32_t LaB = fbits(fmaxf(La, 0.f)), HaB = fbits(fmaxf(Ha, 0.f));
       const uint32_t hrow = (uint32_t)upper << 2;
       uint32_t belowx = 0;
       const f32x16 zero = {};
-      while (ha) {
+      const float *pts = W.G.pts;
+      bool more = true;  // the stream has not ended (the last tile built existed)
+      // build the next pair and issue its loads (unconditionally) into (h, v, p) of a set
+      auto build_pair = [&](bool &ha_, bool &va_, f32x3 &pa_, bool &hb_, bool &vb_, f32x3 &pb_)
+                            __attribute__((always_inline)) {
+        uint32_t i0 = 0, i1 = 0;
+        bool v0 = false, v1 = false;
+        const bool h0 = more && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, i0, v0);
+        const bool h1 = h0 && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, i1, v1);
+        more = h1;
+        pa_ = ld_point(pts, h0 ? i0 : 0u);
+        pb_ = ld_point(pts, h1 ? i1 : 0u);
+        ha_ = h0;
+        va_ = v0;
+        hb_ = h1;
+        vb_ = v1;
+      };
+      auto step = [&](bool &ha, bool &va, f32x3 &pa, bool &hb, bool &vb, f32x3 &pb) __attribute__((always_inline)) {
+        wait_vm2(pa, pb);  // this pair's loads (the other set's two are younger)
+        const float pax = pa.x, pay = pa.y, paz = pa.z, pbx = pb.x, pby = pb.y, pbz = pb.z;
         // tile A and tile B (dummy rows, and a missing tile B: |p|² = 8, far above any band)
         const float ax = va ? (pax - cx) * S : 0.f, ay = va ? (pay - cy) * S : 0.f, az = va ? (paz - cz) * S : 0.f;
         f16x8 fa = frag_a(ax, ay, az, upper);
@@ -602,24 +657,10 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
           stage[96 + 3 * j + 2] = pbz;
         }
         evals += hb ? 64u : 32u;
-        // the next pair: built and its loads issued under the MFMAs
-        uint32_t ic = 0, id = 0;
-        bool vc = false, vd = false;
-        // (both tiles are built before either's loads are issued: a cell change inside the
+        // this set's registers take the pair after the other set's (built under the MFMAs;
+        // both tiles are built before either's loads are issued: a cell change inside the
         // builder waits for the slot loads, and with them for every older load)
-        const bool hc = hb && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, ic, vc);
-        const bool hd = hc && next_tile(W, I, S_, o1, o2, o3, b0, b1, b2, b3, id, vd);
-        float pcx = 0.f, pcy = 0.f, pcz = 0.f, pdx = 0.f, pdy = 0.f, pdz = 0.f;
-        if (hc) {
-          pcx = W.G.pts[3ull * ic];
-          pcy = W.G.pts[3ull * ic + 1];
-          pcz = W.G.pts[3ull * ic + 2];
-        }
-        if (hd) {
-          pdx = W.G.pts[3ull * id];
-          pdy = W.G.pts[3ull * id + 1];
-          pdz = W.G.pts[3ull * id + 2];
-        }
+        build_pair(ha, va, pa, hb, vb, pb);
         // per value 4 VALU, no lane masks: the sign of (a - La) / (a - Ha) on the float bits
         // (a >= 0 by the bias) shifted into two bit masks with v_alignbit; bit r < 16:
         // tile A value r, bit 16 + r: tile B value r
@@ -638,20 +679,24 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
         }
         below += (uint32_t)__builtin_popcount(ltL);
         uint32_t bits = ltH & ~ltL;
+        // (the counters as locals: captured by reference, the two increments below became
+        // one store through a selected pointer, in scratch)
+        uint32_t nbx = belowx, nc = cnt;
         if (LSK_MF_EXP & 2) {
-          belowx += __builtin_popcount(bits);
+          nbx += __builtin_popcount(bits);
           bits = 0;
         }
-        // band candidates, two per round (rounds = the wave's largest count / 2)
+        // band candidates, two per round (rounds = the wave's largest count / 2), branch
+        // free: a candidate that is not in the band stores into the query's pad dword
         while (__ballot(bits != 0u)) {
 #ifdef LSK_MF_PROFILE
           prof[4]++;
 #endif
           const bool h0 = bits != 0u;
-          const uint32_t r0 = h0 ? (uint32_t)__builtin_ctz(bits) : 0u;
+          const uint32_t r0 = (uint32_t)__builtin_ctz(bits | 0x80000000u);
           bits &= bits - 1u;
           const bool h1 = bits != 0u;
-          const uint32_t r1 = h1 ? (uint32_t)__builtin_ctz(bits) : 0u;
+          const uint32_t r1 = (uint32_t)__builtin_ctz(bits | 0x80000000u);
           bits &= bits - 1u;
           // staged point of value r: tile (r >> 4), row (r & 3) + 8 ((r >> 2) & 3) + 4 h
           const uint32_t q0 = r0 & 15u, q1 = r1 & 15u;
@@ -660,36 +705,37 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
           const float e0 = lsk::dist2(qx - stage[w0], qy - stage[w0 + 1], qz - stage[w0 + 2]);
           const float e1 = lsk::dist2(qx - stage[w1], qy - stage[w1 + 1], qz - stage[w1 + 2]);
           const uint32_t eb0 = fbits(e0), eb1 = fbits(e1);
-          if (h0) {
-            if (eb0 < Lb) {
-              belowx++;
-            } else if (eb0 < Hb) {
-              const uint32_t pos = upper ? kCapQ - 1u - min(cnt, kCapQ - 1u) : min(cnt, kCapQ - 1u);
-              region[j * kStride + pos] = eb0;
-              cnt++;
-            }
-          }
-          if (h1) {
-            if (eb1 < Lb) {
-              belowx++;
-            } else if (eb1 < Hb) {
-              const uint32_t pos = upper ? kCapQ - 1u - min(cnt, kCapQ - 1u) : min(cnt, kCapQ - 1u);
-              region[j * kStride + pos] = eb1;
-              cnt++;
-            }
-          }
+          const bool lo0 = h0 && eb0 < Lb, lo1 = h1 && eb1 < Lb;
+          const bool in0 = h0 && !lo0 && eb0 < Hb, in1 = h1 && !lo1 && eb1 < Hb;
+          nbx += (uint32_t)lo0 + (uint32_t)lo1;
+          const uint32_t c0 = min(nc, kCapQ - 1u);
+          nc += (uint32_t)in0;
+          const uint32_t c1 = min(nc, kCapQ - 1u);
+          nc += (uint32_t)in1;
+#if LSK_MF_GBAND
+          if (in0) BAND(j, upper ? kCapQ - 1u - c0 : c0) = eb0;
+          if (in1) BAND(j, upper ? kCapQ - 1u - c1 : c1) = eb1;
+#else
+          const uint32_t qb = j * kStride;
+          region[qb + (in0 ? (upper ? kCapQ - 1u - c0 : c0) : kCapQ)] = eb0;
+          region[qb + (in1 ? (upper ? kCapQ - 1u - c1 : c1) : kCapQ)] = eb1;
+#endif
         }
-        ha = hc;
-        va = vc;
-        pax = pcx;
-        pay = pcy;
-        paz = pcz;
-        hb = hd;
-        vb = vd;
-        pbx = pdx;
-        pby = pdy;
-        pbz = pdz;
+        belowx = nbx;
+        cnt = nc;
+      };
+      bool hxa, vxa, hxb, vxb, hya, vya, hyb, vyb;
+      f32x3 xa, xb, ya, yb;
+      build_pair(hxa, vxa, xa, hxb, vxb, xb);
+      build_pair(hya, vya, ya, hyb, vyb, yb);
+      while (hxa) {
+        step(hxa, vxa, xa, hxb, vxb, xb);
+        if (!hya) break;
+        step(hya, vya, ya, hyb, vyb, yb);
       }
+      // the loads still in flight land in registers nothing reads again: keep all four
+      // live up to a full drain, so no other value takes them while a load is pending
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(xa), "+v"(xb), "+v"(ya), "+v"(yb) : : "memory");
       const uint32_t pcnt = partner_u(cnt);
       const bool ovf = cnt + pcnt > kCapQ;
       const uint32_t kept = min(cnt, kCapQ);
@@ -743,6 +789,9 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
         }
       }
       // ---- selection of the m-th exact band value (m = k - below, 1-based)
+#if LSK_MF_GBAND
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the band stores are done
+#endif
       if (__ballot(sel)) {
         uint32_t m = sel ? k - btot : 1u;
         uint32_t lo = Lb, w = Hb - Lb;
@@ -763,7 +812,7 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
             kmax = lsk::uniform(kmax);
             for (uint32_t e = 0; e < kmax; e++) {
               if (more && e < km) {
-                const uint32_t v = region[j * kStride + (upper ? kCapQ - 1u - e : e)];
+                const uint32_t v = BAND(j, (upper ? kCapQ - 1u - e : e));
                 const uint32_t d = v - lo;
                 if (d < w) {
                   const uint32_t sb = d >> sh;
@@ -804,15 +853,18 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
           kmax = lsk::uniform(kmax);
           for (uint32_t e = 0; e < kmax; e++) {
             if (sel && e < km) {
-              const uint32_t v = region[j * kStride + (upper ? kCapQ - 1u - e : e)];
+              const uint32_t v = BAND(j, (upper ? kCapQ - 1u - e : e));
               if (v - lo < w) {
-                region[j * kStride + (upper ? kCapQ - 1u - mine : mine)] = v;
+                BAND(j, (upper ? kCapQ - 1u - mine : mine)) = v;
                 mine++;
               }
             }
           }
         }
         const uint32_t other = partner_u(mine);
+#if LSK_MF_GBAND
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partner's compaction stores
+#endif
         if (sel && !upper) {
           if (w <= 1u || mine + other > 32u) {
             // all equal (w == 1) or still crowded (pathological ties): lo is exact for w == 1
@@ -829,8 +881,7 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
 #pragma unroll
             for (int i = 0; i < 32; i++) {
               const uint32_t ui = (uint32_t)i;
-              v[i] = ui < mine ? region[j * kStride + ui]
-                               : (ui < mine + other ? region[j * kStride + kCapQ - 1u - (ui - mine)] : 0xffffffffu);
+              v[i] = ui < mine ? BAND(j, ui) : (ui < mine + other ? BAND(j, kCapQ - 1u - (ui - mine)) : 0xffffffffu);
             }
             uint32_t r;
             net32_select(v, m, r);
@@ -915,12 +966,24 @@ extern "C" int lsk_hip_knn_mfma(const lsk_knn_args *args, const lsk_grid_view *g
   const int64_t gend = A.wave_end > 0 && A.wave_end < ngroups ? A.wave_end : ngroups;
   if (A.wave_base < 0 || gend - A.wave_base <= 0) return 0;
   const unsigned nblk = lsk_blocks(gend - A.wave_base, 1);
+#if LSK_MF_GBAND
+  // (tuning build only: one static buffer, not safe for concurrent launches)
+  static uint32_t *gband = nullptr;
+  if (!gband) LSK_HIP(hipMalloc(&gband, (size_t)kStrideBlocksFull * kWPB * kQ * kCapQ * sizeof(uint32_t)));
+  {
+    const unsigned cap = kStrideBlocksFull;
+    unsigned nb = nblk < cap ? nblk : cap;
+    if (nb >= 8u) nb &= ~7u;
+    knn_mfma_kernel<true><<<nb, kThreads, 0, (hipStream_t)stream>>>(A, *grid, gband);
+  }
+#else
   if (A.pad2 >= 1) {
     const unsigned cap = A.pad2 == 2 ? kStrideBlocksFull : kStrideBlocks;
-    knn_mfma_kernel<true><<<nblk < cap ? nblk : cap, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+    knn_mfma_kernel<true><<<nblk < cap ? nblk : cap, kThreads, 0, (hipStream_t)stream>>>(A, *grid, nullptr);
   } else {
-    knn_mfma_kernel<false><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+    knn_mfma_kernel<false><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A, *grid, nullptr);
   }
+#endif
   LSK_CHECK_LAUNCH("knn_mfma");
   return 0;
 }
