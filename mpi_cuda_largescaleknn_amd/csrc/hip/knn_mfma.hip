@@ -152,6 +152,9 @@ constexpr uint32_t kOnes16 = 0x3C003C00u;  // (1.0, 1.0) in f16
 // Point loads the compiler does not see as loads: issued unconditionally (it cannot sink a
 // load into the one path that uses it, which would leave other paths with fewer younger
 // loads and force vmcnt(0)), waited for by hand with a count that holds on every path.
+// Valid only in a build without VGPR spills (the compiler could spill the destination
+// before the hand-placed wait): the production build has none (MINW 3); a MINW 6 probe
+// with 58 spilled VGPRs faulted (profiles/r5_mfma/occupancy_gband.log).
 typedef float f32x3 __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ f32x3 ld_point(const float *pts, uint32_t i) {
   f32x3 v;

@@ -15,9 +15,11 @@ Device selection follows the reference's ``-g G`` (device = rank % G,
 unorderedDataVariant.cu:138-143); without ``-g`` the local rank picks the device
 (the reference would put every rank on GPU 0).
 
-The process group is RCCL (``nccl``) for GPU runs and gloo for CPU runs.
-``LSKNN_DIST_BACKEND=rccl`` uses the native RCCL communicator instead (parallel/rccl.py:
-RCCL called from C++ on the pipeline's own streams; a gloo group for control).
+GPU runs move data with RCCL: by default the native communicator (``rccl``,
+parallel/rccl.py: RCCL 2.27 called from C++ on the pipeline's own streams, a gloo group
+for control; measured faster than torch's group, default_gpu_backend), or torch's
+ProcessGroupNCCL (``LSKNN_DIST_BACKEND=nccl``, torch's bundled RCCL 2.26). CPU runs use
+gloo.
 ``LSKNN_DIST_BACKEND=mpi`` moves the data with MPI (parallel/mpi.py, the native host-staged
 communicator; launch with mpirun).
 ``LSKNN_DIST_BACKEND=gloo`` forces gloo with GPU data (collectives staged through host
@@ -93,6 +95,20 @@ def pick_device(rank: int, local: int, ndev: int, gpu_affinity: int = 0,
     return local % max(1, ndev)
 
 
+def default_gpu_backend() -> str:
+    """The GPU data path when LSKNN_DIST_BACKEND is unset: "rccl" (the native communicator,
+    parallel/rccl.py, on ROCm's RCCL 2.27) when its library is built and an RCCL library
+    is present, else "nccl" (torch's ProcessGroupNCCL on its bundled RCCL 2.26). Measured
+    on a forced 1-rank group, 1e8 points, stream of sets: native 1056.2 / 1058.9 Mpts/s
+    against torch 1036.2 / 1042.3 (alltoallv of the points 0.94-0.97 ms against 1.27-1.28;
+    profiles/r5_rccl_ab/); 2.27 also carries the fix for the > 1 GiB corruption that
+    comm.MAX_MSG_BYTES works around on 2.26. The answer depends only on files of the
+    image, so every rank of a job makes the same choice."""
+    from .. import _build
+    from .rccl import rccl_path
+    return "rccl" if os.path.exists(_build.COMM_LIB) and os.path.exists(rccl_path()) else "nccl"
+
+
 def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False,
          force_distributed: bool | None = None, bootstrap: str = "auto",
          device_map: list[int] | None = None) -> Launch:
@@ -130,7 +146,7 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         # collective timeout = watchdog timeout; RCCL errors surface asynchronously
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = datetime.timedelta(seconds=F.timeout_s())
-        backend = os.environ.get("LSKNN_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+        backend = os.environ.get("LSKNN_DIST_BACKEND") or (default_gpu_backend() if use_gpu else "gloo")
         if backend not in ("nccl", "gloo", "rccl", "mpi"):
             raise ValueError(f"LSKNN_DIST_BACKEND must be nccl, rccl, gloo or mpi, not {backend!r}")
         if backend == "mpi":

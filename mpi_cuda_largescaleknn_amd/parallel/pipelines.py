@@ -690,71 +690,6 @@ HALO_ONE_RANK = os.environ.get("LSKNN_HALO_ONE_RANK", "0") == "1"
 # tests: streamed redistribution also for device-resident input (env LSKNN_FORCE_STREAM=1)
 FORCE_STREAM = os.environ.get("LSKNN_FORCE_STREAM", "0") == "1"
 
-# Single rank, host input, LSKNN_UPLOAD_CHUNK > 0: the points go to the device in chunks
-# on a copy stream and each chunk's bounds and curve keys are computed as it lands, under
-# the rest of the copy (the keys use the first chunk's box widened by UPLOAD_MARGIN of its
-# extent; if any point falls outside it, a device-side flag re-keys everything with the
-# exact box — no host round trip, so the step stays capturable as one HIP graph). Exact
-# either way: keys only order the points. Off by default: on the 1B bench it hides the
-# 9 ms of bounds + keys but the chunked copies run slower than one 12 GB copy
-# (1583-1585 ms per step with one copy; 1595-1600 ms with 16M / 64M / 128M-point chunks;
-# profiles/archive/r2_upload).
-UPLOAD_CHUNK = int(os.environ.get("LSKNN_UPLOAD_CHUNK", "0"))
-UPLOAD_MARGIN = 0.02
-_COPY_STREAMS: dict = {}
-
-
-def _copy_stream(dev: torch.device):
-    import threading
-    key = (threading.get_ident(), dev.index)
-    st = _COPY_STREAMS.get(key)
-    if st is None:
-        st = _COPY_STREAMS[key] = torch.cuda.Stream(dev)
-    return st
-
-
-def upload_keyed(host_pts: torch.Tensor, dev: torch.device, chunk: int | None = None):
-    """-> (device points, (keys, iota), exact box) for build_index(keys=...)."""
-    n = host_pts.shape[0]
-    chunk = max(1, int(chunk or UPLOAD_CHUNK))
-    cur = torch.cuda.current_stream(dev)
-    cp = _copy_stream(dev)
-    pts = torch.empty((n, 3), dtype=torch.float32, device=dev)
-    keys = torch.empty(n, dtype=torch.int32, device=dev)
-    iota = torch.empty(n, dtype=torch.int32, device=dev)
-    spans = [(s, min(s + chunk, n)) for s in range(0, n, chunk)]
-    cp.wait_stream(cur)
-    events = []
-    for s, e in spans:
-        with torch.cuda.stream(cp):
-            pts[s:e].copy_(host_pts[s:e], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(cp)
-        events.append(ev)
-    lo = hi = prov = None
-    for c, (s, e) in enumerate(spans):
-        cur.wait_event(events[c])
-        b = K.bounds(pts[s:e])
-        if c == 0:
-            lo, hi = b[0:3].clone(), b[3:6].clone()
-            ext = (hi - lo).amax() * UPLOAD_MARGIN
-            prov = torch.zeros(8, dtype=torch.float32, device=dev)
-            prov[0:3] = lo - ext
-            prov[3:6] = hi + ext
-            prov = K.box_finalize(prov)
-        else:
-            lo = torch.minimum(lo, b[0:3])
-            hi = torch.maximum(hi, b[3:6])
-        K.morton_into(pts[s:e], prov, keys[s:e], iota[s:e], s)
-    box = torch.zeros(8, dtype=torch.float32, device=dev)
-    box[0:3] = lo
-    box[3:6] = hi
-    box = K.box_finalize(box)
-    outside = ((lo < prov[0:3]).any() | (hi > prov[3:6]).any()).to(torch.int32).reshape(1)
-    K.morton_into(pts, box, keys, None, 0, flag=outside)
-    return pts, (keys, iota), box
-
-
 def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int,
                 info: RunInfo | None = None, pre: tuple | None = None) -> tuple[E.LocalIndex, float | torch.Tensor]:
     """Single-rank first half: points (host or device) -> device, bounds, radius hint,
@@ -768,9 +703,6 @@ def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int
     n_local = points.shape[0]
     if pre is not None:
         box, keys = pre[0], (pre[1], None)
-    elif points.device.type == "cpu" and dev.type == "cuda" and n_local > 0 and UPLOAD_CHUNK > 0:
-        dpts, keys, box = upload_keyed(points, dev)
-        points = dpts
     else:
         points = points.to(dev, non_blocking=True) if points.device != dev else points
         box, keys = global_box(points, comm), None

@@ -13,8 +13,9 @@ Which RCCL: `LSKNN_RCCL_LIB` (a path), else ROCm's /opt/rocm/lib/librccl.so.1 (2
 else torch's bundled copy (2.26). The library is dlopen'ed by path with local symbols, so
 it does not clash with the copy torch itself loaded.
 
-Select it with ``LSKNN_DIST_BACKEND=rccl`` (launch.init); TorchComm ("nccl") stays the
-default.
+It is the default GPU data path of a multi-rank run (launch.default_gpu_backend: faster
+than TorchComm on a forced 1-rank group, profiles/r5_rccl_ab/); ``LSKNN_DIST_BACKEND=nccl``
+selects torch's ProcessGroupNCCL instead.
 """
 from __future__ import annotations
 

@@ -10,5 +10,9 @@ run() {  # run <timeout> <log> <cmd...>
   echo "   rc=$rc" | tee -a gpurun_out/summary.log
   tail -5 "gpurun_out/$log" | tee -a gpurun_out/summary.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: rc=$rc" | tee -a gpurun_out/summary.log; exit $rc; fi
+  # a GPU fault can surface as a Python exception (rc 1): stop before anything else runs
+  if grep -qE "MEMORY_APERTURE_VIOLATION|illegal memory access|HSA_STATUS_ERROR|Memory access fault" "gpurun_out/$log"; then
+    echo "STOP: GPU fault reported in $log" | tee -a gpurun_out/summary.log; exit 3
+  fi
   return 0
 }

@@ -244,30 +244,3 @@ def test_streamed_uneven_ranks_gpu(sizes, monkeypatch):
         return out.clone()
 
     assert torch.equal(torch.cat(run_loopback(3, fn, DEV)), ref)
-
-
-@pytest.mark.parametrize("sorted_x", [False, True])
-def test_single_rank_streamed_upload(sorted_x, monkeypatch):
-    """One rank, pinned host input: chunks are copied on a copy stream and keyed as they
-    land (provisional box of the first chunk). Input sorted along x makes the first chunk
-    unrepresentative: the device-side flag re-keys with the exact box (keys then equal
-    the exact-box keys). Results bit-identical to device input either way."""
-    from mpi_cuda_largescaleknn_amd.parallel.comm import SingleComm
-    monkeypatch.setattr(PL, "UPLOAD_CHUNK", 50_000)
-    p = clustered(300_000, seed=9)
-    if sorted_x:
-        p = p[torch.argsort(p[:, 0])].contiguous()
-    host = torch.empty_like(p).pin_memory()
-    host.copy_(p)
-    cfg = E.KnnConfig(k=60)
-    comm = SingleComm(DEV)
-    ref = PL.unordered_knn(p.to(DEV), comm, cfg).cpu()
-    got = PL.unordered_knn(host, comm, cfg).cpu()
-    assert torch.equal(got, ref)
-    dpts, (keys, iota), box = PL.upload_keyed(host, DEV)
-    torch.cuda.synchronize()
-    assert torch.equal(dpts.cpu(), p)
-    assert torch.equal(iota.cpu(), torch.arange(p.shape[0], dtype=torch.int32))
-    assert torch.equal(box.cpu(), K.bounds(p.to(DEV)).cpu())
-    if sorted_x:
-        assert torch.equal(keys.cpu(), K.morton(p.to(DEV), box)[0].cpu())

@@ -63,3 +63,16 @@ def test_unknown_backend_rejected(monkeypatch):
         for k in set(os.environ) - set(saved):
             del os.environ[k]
         os.environ.update(saved)
+
+
+def test_default_gpu_backend(monkeypatch):
+    """The native communicator is the GPU default when its library and an RCCL are on
+    disk (the measured-faster path), torch's group otherwise; the choice depends only on
+    files, so every rank of a job makes the same one."""
+    from mpi_cuda_largescaleknn_amd import _build
+    from mpi_cuda_largescaleknn_amd.parallel import launch as LA
+    real = os.path.exists
+    monkeypatch.setattr(os.path, "exists", lambda p: True if p in (_build.COMM_LIB, R.rccl_path()) else real(p))
+    assert LA.default_gpu_backend() == "rccl"
+    monkeypatch.setattr(os.path, "exists", lambda p: False if p == _build.COMM_LIB else real(p))
+    assert LA.default_gpu_backend() == "nccl"
