@@ -71,8 +71,8 @@ def test_default_gpu_backend(monkeypatch):
     files, so every rank of a job makes the same one."""
     from mpi_cuda_largescaleknn_amd import _build
     from mpi_cuda_largescaleknn_amd.parallel import launch as LA
-    real = os.path.exists
-    monkeypatch.setattr(os.path, "exists", lambda p: True if p in (_build.COMM_LIB, R.rccl_path()) else real(p))
+    real, lib = os.path.exists, R.rccl_path()
+    monkeypatch.setattr(os.path, "exists", lambda p: True if p in (_build.COMM_LIB, lib) else real(p))
     assert LA.default_gpu_backend() == "rccl"
     monkeypatch.setattr(os.path, "exists", lambda p: False if p == _build.COMM_LIB else real(p))
     assert LA.default_gpu_backend() == "nccl"
