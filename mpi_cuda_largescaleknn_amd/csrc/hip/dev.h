@@ -71,6 +71,21 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
+// Blocks of a launch that have work. A launch over a group list whose length is counted
+// on the device (A.groups + A.ngroups_dev: a rank's interior / boundary groups) is sized by
+// the list's bound and most of its tail blocks return at once; remapping over the whole
+// grid would give the XCDs holding the tail ranges almost nothing to do (a 95 % list: the
+// other XCDs carry 0.125 of the work each instead of 0.119). Blocks at or past the result
+// must return without work (the remap is a bijection on [0, result) only).
+template <class Args>
+__device__ __forceinline__ uint32_t list_blocks(const Args &A, uint32_t nblk, uint32_t waves_per_block) {
+  if (!(A.groups && A.ngroups_dev)) return nblk;
+  const uint64_t cnt = min((uint64_t)A.ngroups, (uint64_t)*A.ngroups_dev);
+  const uint64_t base = (uint32_t)A.wave_base;
+  const uint64_t need = cnt > base ? (cnt - base + waves_per_block - 1) / waves_per_block : 0;
+  return (uint32_t)min(need, (uint64_t)nblk);
+}
+
 }  // namespace lsk
 
 // -------------------------------------------------------------------- host-side errors

@@ -715,7 +715,9 @@ __global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
   if (!STRIDE) {
-    const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t nb = lsk::list_blocks(A, gridDim.x, kWPB);
+    if (blockIdx.x >= nb) return;
+    const uint32_t blk = lsk::xcd_remap(blockIdx.x, nb);
     const uint64_t wave = (uint64_t)blk * kWPB + wid + (uint32_t)A.wave_base;
 #include "knn_grid_wave.inc"
   } else {

@@ -450,8 +450,10 @@ __global__ __launch_bounds__(kThreads, LSK_MF_MINW) void knn_mfma_kernel(const l
   uint64_t gend = ngroups;
   if (A.groups && A.ngroups_dev) gend = min(gend, (uint64_t)*A.ngroups_dev);
   if (A.wave_end > 0) gend = min(gend, (uint64_t)A.wave_end);
+  const uint32_t nb = STRIDE ? gridDim.x : lsk::list_blocks(A, gridDim.x, 1u);
+  if (blockIdx.x >= nb) return;
   uint64_t g = STRIDE ? (uint64_t)blockIdx.x + (uint32_t)A.wave_base
-                      : (uint64_t)lsk::xcd_remap(blockIdx.x, gridDim.x) + (uint32_t)A.wave_base;
+                      : (uint64_t)lsk::xcd_remap(blockIdx.x, nb) + (uint32_t)A.wave_base;
   uint64_t gstep = gridDim.x;
 #if LSK_MF_GBAND
   // persistent blocks, XCD-aware: the blocks of XCD x (blockIdx % 8, the dispatch order)

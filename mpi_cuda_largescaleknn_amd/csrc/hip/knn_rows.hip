@@ -1050,7 +1050,9 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
   if (!STRIDE) {
-    const uint32_t blk = lsk::xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t nb = lsk::list_blocks(A, gridDim.x, kWavesPerBlock);
+    if (blockIdx.x >= nb) return;
+    const uint32_t blk = lsk::xcd_remap(blockIdx.x, nb);
     const uint64_t wave = (uint64_t)blk * kWavesPerBlock + wid + (uint32_t)A.wave_base;
 #include "knn_rows_wave.inc"
   } else {

@@ -116,6 +116,15 @@ for r in range(P):
         E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng, ngroups_dev=icnt)
 
     _, t_local = timed(local)
+    # the two launches apart, and the whole rank in one launch without lists (the kernel's
+    # own time at this density: what the split costs)
+    _, t_bnd = timed(lambda: E.query(index, cfg, hint2, out=d2, final_out=fin, groups=blist, ngroups=ng,
+                                     ngroups_dev=bcnt, short_list=True))
+    _, t_int = timed(lambda: E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng,
+                                     ngroups_dev=icnt))
+    d2_all = torch.empty(nr, dtype=torch.float32, device=DEV)
+    _, t_all = timed(lambda: E.query(index, cfg, hint2, out=d2_all, final_out=fin))
+    del d2_all
     # what this rank sends: its points against the other ranks' exact published radii
     pub2, dep2, off2 = st["pubs"][1]
     mask, t_mask = timed(lambda: K.halo_mask(index.pts[:nr], pub2.reshape(-1), off2, dep2, r))
@@ -138,6 +147,8 @@ for r in range(P):
            "local_ms": round(t_local, 2), "halo_ms": round(t_mask + t_htree, 2), "requery_ms": round(t_req, 2),
            "return_ms": round(t_ret, 2)}
     row["total_ms"] = round(sum(v for kk, v in row.items() if kk.endswith("_ms")), 2)
+    row["local_split"] = {"boundary_ms": round(t_bnd, 2), "interior_ms": round(t_int, 2),
+                          "one_launch_no_lists_ms": round(t_all, 2)}
     row["grid"] = index.grid.decision() if index.grid is not None else None
     rows.append(row)
     print(json.dumps(row), flush=True)
