@@ -18,7 +18,10 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / lsk::kWave;
 constexpr int kRadix = 256;
-constexpr int kRows = 16;  // rows of 64 per wave per tile (8: 36.5 vs 33.6 ms for 1B keys)
+#ifndef LSK_SORT_ROWS
+#define LSK_SORT_ROWS 16
+#endif
+constexpr int kRows = LSK_SORT_ROWS;  // rows of 64 per wave per tile (8: 36.5 vs 33.6 ms for 1B keys)
 constexpr int kTile = kWaves * lsk::kWave * kRows;     // 4096 elements
 constexpr unsigned kMaxBlocks = 2048;
 

@@ -146,7 +146,8 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
         # collective timeout = watchdog timeout; RCCL errors surface asynchronously
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = datetime.timedelta(seconds=F.timeout_s())
-        backend = os.environ.get("LSKNN_DIST_BACKEND") or (default_gpu_backend() if use_gpu else "gloo")
+        chosen = os.environ.get("LSKNN_DIST_BACKEND")
+        backend = chosen or (default_gpu_backend() if use_gpu else "gloo")
         if backend not in ("nccl", "gloo", "rccl", "mpi"):
             raise ValueError(f"LSKNN_DIST_BACKEND must be nccl, rccl, gloo or mpi, not {backend!r}")
         if backend == "mpi":
@@ -174,7 +175,29 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
             from .rccl import RcclComm
             dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
             store = dist.distributed_c10d._get_default_store()
-            comm = RcclComm(device, rank, size, store, force=force_distributed)
+            try:
+                comm, err = RcclComm(device, rank, size, store, force=force_distributed), None
+            except Exception as e:  # noqa: BLE001 (decided together below)
+                comm, err = None, e
+            if chosen is None:
+                # the default, not the user's choice: if any rank could not bring the native
+                # communicator up, every rank falls back to torch's group (agreed over gloo)
+                ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) == 0:
+                    if comm is not None:
+                        comm.destroy(abort=True)
+                    if rank == 0:
+                        print(f"lsknn: native RCCL communicator unavailable ({err or 'on another rank'}); "
+                              "using torch's process group", flush=True)
+                    opts = dist.ProcessGroupNCCL.Options()
+                    opts.is_high_priority_stream = True
+                    group = dist.new_group(backend="nccl", pg_options=opts)
+                    comm = TorchComm(device, group=group, force=force_distributed)
+                    watchdog = F.Watchdog(rank, size, store).start()
+                    return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
+            elif comm is None:
+                raise err
             watchdog = F.Watchdog(rank, size, store, comm_check=comm.async_error, on_abort=comm.abort).start()
             return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
         if backend == "nccl":

@@ -117,6 +117,28 @@ def test_bench_forced_rccl_single_gpu(backend):
     assert v and v.split(".")[0] == "2", rec["config"]["comm_info"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("lib", ["default", "broken"])
+def test_bench_default_backend_single_gpu(lib):
+    """No LSKNN_DIST_BACKEND: the native communicator is the GPU data path; if it cannot
+    come up (here: LSKNN_RCCL_LIB names a file that is no RCCL library) every rank agrees
+    over gloo to fall back to torch's RCCL group, and the run still completes."""
+    env = dict(_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.pop("LSKNN_DIST_BACKEND", None)
+    if lib == "broken":
+        env["LSKNN_RCCL_LIB"] = os.path.join(ROOT, "bench.py")
+    out = subprocess.run([sys.executable, "bench.py", "--points", "300000", "--steps", "2", "--warmup", "1",
+                          "--force-dist", "--pipeline", "0"], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_line(out.stdout)
+    assert rec["config"]["sampled_exact"] == "256/256"
+    want = "rccl" if lib == "default" else "nccl"
+    assert rec["config"]["comm_info"]["backend"] == want, rec["config"]["comm_info"]
+    if lib == "broken":
+        assert "native RCCL communicator unavailable" in out.stdout + out.stderr
+
+
 @pytest.mark.parametrize("variant", ["unordered", "prepartitioned"])
 def test_bench_two_ranks_torchrun_gloo(variant):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
