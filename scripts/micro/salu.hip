@@ -14,14 +14,14 @@ __global__ __launch_bounds__(256) void k(uint32_t *out, int iters) {
   for (int it = 0; it < iters; it++) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      if (NS >= 1) asm volatile("s_add_u32 %0, %0, 1" : "+s"(s0));
-      if (NS >= 2) asm volatile("s_add_u32 %0, %0, 3" : "+s"(s1));
-      if (NS >= 3) asm volatile("s_add_u32 %0, %0, 5" : "+s"(s2));
-      if (NS >= 4) asm volatile("s_add_u32 %0, %0, 7" : "+s"(s3));
-      if (NS >= 5) asm volatile("s_add_u32 %0, %0, 9" : "+s"(s4));
-      if (NS >= 6) asm volatile("s_add_u32 %0, %0, 11" : "+s"(s5));
-      if (NS >= 7) asm volatile("s_add_u32 %0, %0, 13" : "+s"(s6));
-      if (NS >= 8) asm volatile("s_add_u32 %0, %0, 15" : "+s"(s7));
+      if (NS >= 1) asm volatile("s_add_u32 %0, %0, 1" : "+s"(s0) : : "scc");
+      if (NS >= 2) asm volatile("s_add_u32 %0, %0, 3" : "+s"(s1) : : "scc");
+      if (NS >= 3) asm volatile("s_add_u32 %0, %0, 5" : "+s"(s2) : : "scc");
+      if (NS >= 4) asm volatile("s_add_u32 %0, %0, 7" : "+s"(s3) : : "scc");
+      if (NS >= 5) asm volatile("s_add_u32 %0, %0, 9" : "+s"(s4) : : "scc");
+      if (NS >= 6) asm volatile("s_add_u32 %0, %0, 11" : "+s"(s5) : : "scc");
+      if (NS >= 7) asm volatile("s_add_u32 %0, %0, 13" : "+s"(s6) : : "scc");
+      if (NS >= 8) asm volatile("s_add_u32 %0, %0, 15" : "+s"(s7) : : "scc");
       if (NV >= 1) asm volatile("v_add_u32 %0, %0, 1" : "+v"(v0));
       if (NV >= 2) asm volatile("v_add_u32 %0, %0, 3" : "+v"(v1));
       if (NV >= 3) asm volatile("v_add_u32 %0, %0, 5" : "+v"(v2));
@@ -55,6 +55,7 @@ int main() {
     (void)hipEventSynchronize(e1);                                                                         \
     (void)hipEventElapsedTime(&ms, e0, e1);                                                                \
     const double waves = (double)cus * (BPC) * 4, cyc = ms * 1e-3 * 2.4e9;                                 \
+    if (hipGetLastError() != hipSuccess) printf("launch error\n");                                    \
     if (rep)                                                                                               \
       printf("NS %d NV %d waves/SIMD %d: %8.3f ms  SALU/CU/cyc %.3f  VALU/SIMD/cyc %.3f\n", NS, NV, BPC, ms, \
              waves / cus * iters * 4 * (NS) / cyc, waves / cus / 4 * iters * 4 * (NV) / cyc);             \

@@ -1,4 +1,6 @@
 """Synthetic point sets for tests (uniform, clustered, degenerate)."""
+import math
+
 import torch
 
 
@@ -26,6 +28,23 @@ def planar(n, seed=0):
     return p
 
 
+def tilted_plane(n, seed=0, angle=0.6):
+    """Uniform points on a plane through the cube's centre, tilted about x (not axis-aligned:
+    every coordinate varies)."""
+    p = uniform(n, seed) - 0.5
+    p[:, 2] = 0.0
+    c, s = math.cos(angle), math.sin(angle)
+    rot = torch.tensor([[1.0, 0.0, 0.0], [0.0, c, -s], [0.0, s, c]])
+    return (p @ rot.T + 0.5).contiguous()
+
+
+def line(n, seed=0):
+    """Uniform points on a segment (1-D data in 3-D)."""
+    g = torch.Generator().manual_seed(seed)
+    t = torch.rand(n, generator=g)
+    return torch.stack([t, 0.3 + 0.2 * t, 0.7 - 0.1 * t], dim=1).contiguous()
+
+
 def lattice(m):
     r = torch.arange(m, dtype=torch.float32) / m
     x, y, z = torch.meshgrid(r, r, r, indexing="ij")
@@ -45,4 +64,6 @@ GENERATORS = {
     "duplicates": duplicates,
     "planar": planar,
     "mixed_scale": mixed_scale,
+    "tilted_plane": tilted_plane,
+    "line": line,
 }
