@@ -6,8 +6,9 @@ Runs SetStream over `sets` alternating sets of n uniform points (pinned host mem
 bench.py) per mode and prints ms per set (after the first two sets):
   copy     production: the result goes to pinned host memory on the output stream
   nocopy   the result stays on the device (wrong for users: measures the copy's share)
-  late     the result copy waits for the NEXT set's build (runs beside its k-NN, not
-           beside its build)
+Measured (profiles/r5_stream/): copy 885-896 ms per set in the steady state; a result
+copy by a narrow-grid kernel of our own (8-32 workgroups, tried in round 5 and removed)
+937-991 ms — the runtime's blit stays.
 """
 import sys
 import time
