@@ -264,6 +264,10 @@ CAPTURED_HEAVY: list = []
 # unrefined cell only costs speed) and the stream reports it once the sets are done.
 _SYNC_FREE = [0]
 DEFERRED_HEAVY: list = []
+# (pinned host copy, event) of the last sync-free build's over-full-cell flag: a stream of
+# sets learns from set i's flag (complete by the time set i+1 is built, so the read does
+# not wait) that its data has over-full cells, and refines the next sets eagerly
+_HEAVY_SEEN: list = [None]
 
 
 class host_sync_free:
@@ -283,6 +287,7 @@ def deferred_heavy_cells(clear: bool = False) -> bool:
     hit = any(bool(f) for f in DEFERRED_HEAVY)
     if clear:
         DEFERRED_HEAVY.clear()
+        _HEAVY_SEEN[0] = None
     return hit
 
 
@@ -309,6 +314,19 @@ def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Te
         CAPTURED_HEAVY.append(heavy_any)
         return perm
     if _SYNC_FREE[0] and K.is_gpu(skeys):
+        prev = _HEAVY_SEEN[0]
+        flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        flag.copy_(heavy_any.reshape(1).to(torch.int32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        _HEAVY_SEEN[0] = (flag, ev)
+        if prev is not None and prev[1].query() and int(prev[0][0]) != 0:
+            # the previous set had over-full cells: refine eagerly (the host read waits for
+            # this stream's queue, not for a flag still in flight)
+            if not bool(heavy_any):
+                return perm
+            LAST_REFINED = True
+            return _refine_heavy_runs(points, skeys, perm)
         DEFERRED_HEAVY.append(heavy_any)
         del DEFERRED_HEAVY[:-1024]
         return perm

@@ -239,3 +239,29 @@ def test_stream_distributed_loopback_gpu(variant, size):
     per_rank = run_loopback(size, fn, dev)
     for i, p in enumerate(S):
         assert torch.equal(torch.cat([per_rank[r][i] for r in range(size)]), oracle(p, k)), i
+
+
+@pytest.mark.gpu
+def test_stream_learns_heavy_cells_gpu():
+    """A stream of sets with over-full key cells (a dense core inside a large box): the
+    first set's build defers the refinement (no host read inside a stream build), later
+    builds see that flag (complete by then) and refine eagerly; every output stays exact."""
+    dev = torch.device("cuda", 0)
+    p = GENERATORS["mixed_scale"](60_000, seed=4)
+    q = GENERATORS["mixed_scale"](60_000, seed=5)
+    S = [p, q, p, q]
+    k = 20
+    ins = [s.pin_memory() for s in S]
+    outs = [torch.empty(s.shape[0], dtype=torch.float32).pin_memory() for s in S]
+    E.deferred_heavy_cells(clear=True)
+    E.LAST_REFINED = False
+    old = E.HEAVY_RUN
+    E.HEAVY_RUN = 512  # (the core's points share one key; a small set still has over-full runs)
+    try:
+        SetStream(SingleComm(dev), E.KnnConfig(k=k)).run(ins, outs)
+    finally:
+        E.HEAVY_RUN = old
+    assert E.LAST_REFINED  # a later set was refined eagerly
+    assert E.deferred_heavy_cells(clear=True)  # the first one was not (reported)
+    for s, o in zip(S, outs):
+        assert torch.equal(o, oracle(s, k))
