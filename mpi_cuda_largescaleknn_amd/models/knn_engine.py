@@ -264,10 +264,14 @@ CAPTURED_HEAVY: list = []
 # unrefined cell only costs speed) and the stream reports it once the sets are done.
 _SYNC_FREE = [0]
 DEFERRED_HEAVY: list = []
-# (pinned host copy, event) of the last sync-free build's over-full-cell flag: a stream of
-# sets learns from set i's flag (complete by the time set i+1 is built, so the read does
-# not wait) that its data has over-full cells, and refines the next sets eagerly
-_HEAVY_SEEN: list = [None]
+# What a stream of sets knows about over-full cells: the flags of its sync-free builds in
+# flight (pinned host copy, event) and the last one known. The first set of a stream, and
+# every set once a known flag says the data has over-full cells, takes the eager check
+# (one host read: refining such a set costs ~55 ms at 5e6 mixed-scale points, leaving it
+# unrefined ~105 s, profiles/r5_stream/heavy_ab_deferred.log, heavy_ab_learned.log); sets after a known clean one stay
+# sync-free.
+_HEAVY_PENDING: list = []
+_HEAVY_KNOWN: list = [None]
 
 
 class host_sync_free:
@@ -287,7 +291,8 @@ def deferred_heavy_cells(clear: bool = False) -> bool:
     hit = any(bool(f) for f in DEFERRED_HEAVY)
     if clear:
         DEFERRED_HEAVY.clear()
-        _HEAVY_SEEN[0] = None
+        _HEAVY_PENDING.clear()
+        _HEAVY_KNOWN[0] = None
     return hit
 
 
@@ -314,22 +319,24 @@ def refine_heavy_cells(points: torch.Tensor, skeys: torch.Tensor, perm: torch.Te
         CAPTURED_HEAVY.append(heavy_any)
         return perm
     if _SYNC_FREE[0] and K.is_gpu(skeys):
-        prev = _HEAVY_SEEN[0]
-        flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
-        flag.copy_(heavy_any.reshape(1).to(torch.int32), non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        _HEAVY_SEEN[0] = (flag, ev)
-        if prev is not None and prev[1].query() and int(prev[0][0]) != 0:
-            # the previous set had over-full cells: refine eagerly (the host read waits for
-            # this stream's queue, not for a flag still in flight)
-            if not bool(heavy_any):
-                return perm
-            LAST_REFINED = True
-            return _refine_heavy_runs(points, skeys, perm)
-        DEFERRED_HEAVY.append(heavy_any)
-        del DEFERRED_HEAVY[:-1024]
-        return perm
+        while _HEAVY_PENDING and _HEAVY_PENDING[0][1].query():  # flags that landed (no wait)
+            _HEAVY_KNOWN[0] = int(_HEAVY_PENDING.pop(0)[0][0]) != 0
+        if _HEAVY_KNOWN[0] is False:
+            flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            flag.copy_(heavy_any.reshape(1).to(torch.int32), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            _HEAVY_PENDING.append((flag, ev))
+            DEFERRED_HEAVY.append(heavy_any)
+            del DEFERRED_HEAVY[:-1024]
+            return perm
+        # first set of the stream, or the data is known to have over-full cells: eager
+        # (the host read waits for this stream's queue)
+        _HEAVY_KNOWN[0] = bool(heavy_any)
+        if not _HEAVY_KNOWN[0]:
+            return perm
+        LAST_REFINED = True
+        return _refine_heavy_runs(points, skeys, perm)
     if not bool(heavy_any):
         return perm
     LAST_REFINED = True

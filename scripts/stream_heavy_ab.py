@@ -26,14 +26,16 @@ hosts = [datasets.GENERATORS[dist](n, seed=s).pin_memory() for s in (11, 12)]
 print(f"{dist}: 2 sets of {n} points ready", flush=True)
 outs = [torch.empty(n, dtype=torch.float32).pin_memory() for _ in range(2)]
 orig = E.refine_heavy_cells
+MODES = os.environ.get("LSK_MODES", "learned,deferred").split(",")
 
 
-def deferred_only(*a, **kw):  # the round-4 behaviour: never learn from the previous set
-    E._HEAVY_SEEN[0] = None
+def deferred_only(*a, **kw):  # the round-4 behaviour: every stream build defers
+    E._HEAVY_PENDING.clear()
+    E._HEAVY_KNOWN[0] = False
     return orig(*a, **kw)
 
 
-for mode in ("learned", "deferred", "learned"):
+for mode in MODES:
     E.refine_heavy_cells = orig if mode == "learned" else deferred_only
     E.deferred_heavy_cells(clear=True)
     E.LAST_REFINED = False

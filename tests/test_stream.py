@@ -244,8 +244,8 @@ def test_stream_distributed_loopback_gpu(variant, size):
 @pytest.mark.gpu
 def test_stream_learns_heavy_cells_gpu():
     """A stream of sets with over-full key cells (a dense core inside a large box): the
-    first set's build defers the refinement (no host read inside a stream build), later
-    builds see that flag (complete by then) and refine eagerly; every output stays exact."""
+    first set's build checks eagerly and refines, and so does every later one (the data
+    is known to have over-full cells); nothing is left unrefined; every output exact."""
     dev = torch.device("cuda", 0)
     p = GENERATORS["mixed_scale"](60_000, seed=4)
     q = GENERATORS["mixed_scale"](60_000, seed=5)
@@ -261,7 +261,24 @@ def test_stream_learns_heavy_cells_gpu():
         SetStream(SingleComm(dev), E.KnnConfig(k=k)).run(ins, outs)
     finally:
         E.HEAVY_RUN = old
-    assert E.LAST_REFINED  # a later set was refined eagerly
-    assert E.deferred_heavy_cells(clear=True)  # the first one was not (reported)
+    assert E.LAST_REFINED
+    assert not E.deferred_heavy_cells(clear=True)
+    for s, o in zip(S, outs):
+        assert torch.equal(o, oracle(s, k))
+
+
+@pytest.mark.gpu
+def test_stream_clean_sets_stay_sync_free_gpu():
+    """Uniform sets: the first build checks eagerly (clean), later builds defer their flag
+    (no host read) and nothing is reported unrefined."""
+    dev = torch.device("cuda", 0)
+    S = [GENERATORS["uniform"](50_000, seed=s) for s in (1, 2, 3)]
+    k = 16
+    ins = [s.pin_memory() for s in S]
+    outs = [torch.empty(s.shape[0], dtype=torch.float32).pin_memory() for s in S]
+    E.deferred_heavy_cells(clear=True)
+    SetStream(SingleComm(dev), E.KnnConfig(k=k)).run(ins, outs)
+    assert E._HEAVY_KNOWN[0] is False or E._HEAVY_PENDING
+    assert not E.deferred_heavy_cells(clear=True)
     for s, o in zip(S, outs):
         assert torch.equal(o, oracle(s, k))
