@@ -409,9 +409,9 @@ __device__ __forceinline__ CellLoad fetch_cell(const GridCtx &G, uint32_t x, uin
 
 template <int MODE>
 __device__ __forceinline__ void count_batch(GridCtx &G) {
-  G.evals += 4u;
+  G.evals += (uint32_t)LSK_GRID_BATCH;
 #ifdef LSK_GRID_PROFILE
-  G.ev_mode[MODE] += 4u;
+  G.ev_mode[MODE] += (uint32_t)LSK_GRID_BATCH;
 #endif
 }
 
@@ -423,6 +423,25 @@ __device__ __forceinline__ void eval4_tail(Lane &s, GridCtx &G, const Batch &b, 
   const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
   update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane, G.trash);
 }
+
+#ifndef LSK_GRID_BATCH
+#define LSK_GRID_BATCH 8  // candidates per scalar-load batch of the cell stream (4 or 8; 8: 1B stream 952.6 -> 941.9-943.3 ms, profiles/r5_kernel_ab)
+#endif
+#if LSK_GRID_BATCH == 8
+struct Batch8 {
+  Batch a, b;
+};
+__device__ __forceinline__ Batch8 load_batch8(lsk::cfloat_p P, uint32_t i) {
+  const lsk::cfloat_p p = P + 3ull * (uint64_t)i;
+  return Batch8{Batch{p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9], p[10], p[11]},
+                Batch{p[12], p[13], p[14], p[15], p[16], p[17], p[18], p[19], p[20], p[21], p[22], p[23]}};
+}
+template <int MODE>
+__device__ __forceinline__ void eval8(Lane &s, GridCtx &G, const Batch8 &b, uint32_t left) {
+  if (left >= 4u) eval4<MODE>(s, G, b.a); else eval4_tail<MODE>(s, G, b.a, left);
+  if (left >= 8u) eval4<MODE>(s, G, b.b); else if (left > 4u) eval4_tail<MODE>(s, G, b.b, left - 4u);
+}
+#endif
 
 // The candidates of one cell as ONE stream over its needed runs of grandchildren, 4 per
 // batch. Slots are in memory order, so a run of needed (or empty) slots is one
@@ -455,7 +474,7 @@ __device__ __forceinline__ void process_cell_stream(Lane &s, GridCtx &G, const C
   uint32_t chk = i + kSegCheck;
   // position after batch i of [.., e): next batch of the segment, else the next segment
   auto advance = [&](uint32_t &ni, uint32_t &ne) -> bool {
-    ni = i + 4u;
+    ni = i + (uint32_t)LSK_GRID_BATCH;
     ne = e;
     if (ni < e) return true;
     if (!need) {
@@ -465,23 +484,39 @@ __device__ __forceinline__ void process_cell_stream(Lane &s, GridCtx &G, const C
     pop(ni, ne);
     return true;
   };
+#if LSK_GRID_BATCH == 8
+  Batch8 A = load_batch8(P, i);
+#else
   Batch A = load_batch(P, i);
+#endif
   for (;;) {
     uint32_t ni, ne;
     bool more = advance(ni, ne);
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+#if LSK_GRID_BATCH == 8
+    Batch8 B = load_batch8(P, ni);
+    __builtin_amdgcn_sched_barrier(0);
+    eval8<MODE>(s, G, A, e - i);
+#else
     Batch B = load_batch(P, ni);
     __builtin_amdgcn_sched_barrier(0);
     if (e - i >= 4u) eval4<MODE>(s, G, A); else eval4_tail<MODE>(s, G, A, e - i);
+#endif
     count_batch<MODE>(G);
     if (!more) break;
     i = ni;
     e = ne;
     more = advance(ni, ne);
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+#if LSK_GRID_BATCH == 8
+    A = load_batch8(P, ni);
+    __builtin_amdgcn_sched_barrier(0);
+    eval8<MODE>(s, G, B, e - i);
+#else
     A = load_batch(P, ni);
     __builtin_amdgcn_sched_barrier(0);
     if (e - i >= 4u) eval4<MODE>(s, G, B); else eval4_tail<MODE>(s, G, B, e - i);
+#endif
     count_batch<MODE>(G);
     if (!more) break;
     i = ni;
