@@ -49,6 +49,9 @@ using lsk::fbits;
 #ifndef LSK_GRID_MINW
 #define LSK_GRID_MINW 7  // waves per SIMD the register budget is sized for
 #endif
+#ifndef LSK_GRID_BATCH
+#define LSK_GRID_BATCH 8  // candidates per scalar-load batch of the cell stream (4 or 8; 8: 1B stream 952.6 -> 941.9-943.3 ms, profiles/r5_kernel_ab)
+#endif
 #ifndef LSK_GRID_WPB
 #define LSK_GRID_WPB 2
 #endif
@@ -424,9 +427,6 @@ __device__ __forceinline__ void eval4_tail(Lane &s, GridCtx &G, const Batch &b, 
   update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane, G.trash);
 }
 
-#ifndef LSK_GRID_BATCH
-#define LSK_GRID_BATCH 8  // candidates per scalar-load batch of the cell stream (4 or 8; 8: 1B stream 952.6 -> 941.9-943.3 ms, profiles/r5_kernel_ab)
-#endif
 #if LSK_GRID_BATCH == 8
 struct Batch8 {
   Batch a, b;
