@@ -364,7 +364,8 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
   }
 }
 
-// Points [i0, i1) of the sorted array, 4 per batch through scalar loads, software
+// Points [i0, i1) of the sorted array (process_segment: 4 per batch; the cell stream:
+// LSK_GRID_BATCH, 8 — half the per-batch scalar work per candidate) through scalar loads, software
 // pipelined: the wait for batch i (lgkmcnt(0): scalar loads may return out of order, so
 // only an empty queue proves a batch complete) comes BEFORE batch i+1's loads are issued,
 // which then fly while batch i is computed. Reads past i1 stay inside the array's
