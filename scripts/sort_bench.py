@@ -1,5 +1,6 @@
 """Index-build pieces alone on N uniform points: curve keys, 4-pass key sort (iota values),
-key census, gather, tree, grid; best of 3 each (events).
+key census, gather, tree, grid; best of 3 each (events); checks the sort's output
+(non-decreasing keys, a permutation, keys[perm] == sorted keys).
 
     python scripts/sort_bench.py [N]"""
 import sys
@@ -36,6 +37,9 @@ def t(fn, reps=3, setup=None):
 # there): every rep sorts a fresh copy of the unsorted keys, or reps 2-3 would sort sorted
 # keys and the gather below would read an identity permutation
 (sk, perm), t_sort = t(lambda kk: K.sort_keys_iota(kk, 30), setup=lambda: keys.clone())
+ok = bool((sk[1:n] >= sk[:n - 1]).all()) and bool((keys[perm[:n].long()] == sk[:n]).all()) \
+    and bool((torch.bincount(perm[:n].long(), minlength=n) == 1).all())
+print(f"sort check: {'ok' if ok else 'WRONG'}", flush=True)
 _, t_census = t(lambda: K.key_census(sk[:n], E.HEAVY_RUN))
 pts, t_gather = t(lambda: K.gather3(p, perm, pad=K.PAD_POINTS))
 _, t_build = t(lambda: E.build_index(p, box, grid=True))
