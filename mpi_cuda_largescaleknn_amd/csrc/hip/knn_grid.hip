@@ -47,7 +47,10 @@ using lsk::bitsf;
 using lsk::fbits;
 
 #ifndef LSK_GRID_MINW
-#define LSK_GRID_MINW 7  // waves per SIMD the register budget is sized for
+// waves per SIMD the register budget is sized for. 6 (80 VGPRs; 132 SGPRs / 52 VGPRs
+// spilled with 8-candidate batches) against 7 (72 VGPRs; 152 / 89 spilled): 1e8 k=100
+// 79.6 -> 77.7 ms (profiles/r5_kernel_ab/minw6_vs_7_1e8.txt)
+#define LSK_GRID_MINW 6
 #endif
 #ifndef LSK_GRID_BATCH
 #define LSK_GRID_BATCH 8  // candidates per scalar-load batch of the cell stream (4 or 8; 8: 1B stream 952.6 -> 941.9-943.3 ms, profiles/r5_kernel_ab)

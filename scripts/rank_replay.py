@@ -122,6 +122,28 @@ for r in range(P):
                                      ngroups_dev=bcnt, short_list=True))
     _, t_int = timed(lambda: E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng,
                                      ngroups_dev=icnt))
+    # the two passes on two streams at once (the interior's workgroups fill the CUs the
+    # boundary pass's tail leaves idle); hi: the boundary pass's stream has the high priority
+    lo_p, hi_p = torch.cuda.Stream.priority_range()
+
+    def local_conc(hi):
+        cur = torch.cuda.current_stream(DEV)
+        sa, sb = torch.cuda.Stream(DEV, priority=hi_p if hi else 0), torch.cuda.Stream(DEV)
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        pend: list = []
+        with torch.cuda.stream(sa):
+            E.query(index, cfg, hint2, out=d2, final_out=fin, groups=blist, ngroups=ng, ngroups_dev=bcnt,
+                    short_list=True, deferred=pend)
+        with torch.cuda.stream(sb):
+            E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng, ngroups_dev=icnt,
+                    deferred=pend)
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+        E.settle(pend)
+
+    _, t_conc = timed(lambda: local_conc(False))
+    _, t_conc_hi = timed(lambda: local_conc(True))
     d2_all = torch.empty(nr, dtype=torch.float32, device=DEV)
     _, t_all = timed(lambda: E.query(index, cfg, hint2, out=d2_all, final_out=fin))
     del d2_all
@@ -148,7 +170,8 @@ for r in range(P):
            "return_ms": round(t_ret, 2)}
     row["total_ms"] = round(sum(v for kk, v in row.items() if kk.endswith("_ms")), 2)
     row["local_split"] = {"boundary_ms": round(t_bnd, 2), "interior_ms": round(t_int, 2),
-                          "one_launch_no_lists_ms": round(t_all, 2)}
+                          "one_launch_no_lists_ms": round(t_all, 2), "two_streams_ms": round(t_conc, 2),
+                          "two_streams_boundary_hi_ms": round(t_conc_hi, 2)}
     row["grid"] = index.grid.decision() if index.grid is not None else None
     rows.append(row)
     print(json.dumps(row), flush=True)
