@@ -56,7 +56,9 @@ using lsk::fbits;
 #define LSK_GRID_BATCH 8  // candidates per scalar-load batch of the cell stream (4 or 8; 8: 1B stream 952.6 -> 941.9-943.3 ms, profiles/r5_kernel_ab)
 #endif
 #ifndef LSK_GRID_WPB
-#define LSK_GRID_WPB 2
+// waves per workgroup: 1 (1e8 k=100 at 6 waves/SIMD: 77.0 ms; 2: 78.1; 4: 79.6,
+// profiles/r5_kernel_ab/wpb_batch_1e8.txt)
+#define LSK_GRID_WPB 1
 #endif
 constexpr int kWPB = LSK_GRID_WPB;
 constexpr int kThreads = kWPB * lsk::kWave;
@@ -621,8 +623,8 @@ __device__ __forceinline__ void process_cell(Lane &s, GridCtx &G, const CellLoad
 // the local spacing: k beyond the local point count, or an estimate far off) is served by
 // one scan of all points when the tree is small, else the wave hands its unresolved
 // queries to the exact backstop (returns false).
-constexpr unsigned kStrideBlocks = 1024;  // persistent form: 2048 waves, 2 per SIMD
-constexpr unsigned kStrideBlocksFull = 4096;  // persistent form over a short group list: 8192
+constexpr unsigned kStrideBlocks = 2048 / kWPB;  // persistent form: 2048 waves, 2 per SIMD
+constexpr unsigned kStrideBlocksFull = 8192 / kWPB;  // persistent form over a short group list: 8192
                                               // waves, the kernel's full occupancy
 constexpr uint32_t kMaxCells = 4096;
 // Candidate budget of a wave, checked before each pass: max(kEvalBudget, kEvalsPerK * k),
