@@ -70,8 +70,10 @@ FILE_FLAGS = {
     # instead of promoting it to (dynamically indexed, hence many) VGPRs
     # max-memory-clause scheduling: 0.1255 vs 0.1265 s on 1e8 points, k=100 (ilp 0.131,
     # iterative-ilp 0.138; same 72 VGPRs; profiles/archive/r2_kernel/README.txt)
-    # candidates arrive in SGPRs: packed-math pairs would need them moved into VGPRs
-    "knn_grid.hip": ["-fno-slp-vectorize"],
+    # candidates arrive in SGPRs: packed-math pairs would need them moved into VGPRs;
+    # iterative-minreg scheduling: 1e8 k=100 74.4 vs 76.8 ms (iterative-maxocc 75.1,
+    # max-memory-clause 77.5, max-ilp 78.1, iterative-ilp 77.4; profiles/r5_kernel_ab/sched_1e8.txt)
+    "knn_grid.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
     # the f16 fragment packing must stay in the explicit cvt_pkrtz / perm form
     "knn_mfma.hip": ["-fno-slp-vectorize"],
     "knn_rows.hip": ["-fno-slp-vectorize", "-mllvm", "-disable-promote-alloca-to-vector",
@@ -94,12 +96,13 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
 
 def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     srcs = _sources("hip", "hip")
-    if not (force or _stale(HIP_LIB, srcs + _headers())):
+    # (this file holds the compile flags: a flag change rebuilds every object)
+    if not (force or _stale(HIP_LIB, srcs + _headers() + [__file__])):
         return HIP_LIB
     hipcc = _hipcc()
     obj_dir = os.path.join(LIB_DIR, "obj")
     os.makedirs(obj_dir, exist_ok=True)
-    hdrs = _headers()
+    hdrs = _headers() + [__file__]
 
     def compile_one(src: str) -> str:
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
