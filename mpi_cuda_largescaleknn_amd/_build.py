@@ -68,8 +68,10 @@ def _run(cmd: list[str]) -> None:
 FILE_FLAGS = {
     # the pass-1 log is a dynamically indexed private array: keep it in scratch memory
     # instead of promoting it to (dynamically indexed, hence many) VGPRs
-    # max-memory-clause scheduling: 0.1255 vs 0.1265 s on 1e8 points, k=100 (ilp 0.131,
-    # iterative-ilp 0.138; same 72 VGPRs; profiles/archive/r2_kernel/README.txt)
+    # iterative-maxocc scheduling (round 5, 2e7 k=100: clustered 595-600 vs 587-588 Mpts/s
+    # with max-memory-clause, planar 1228-1246 vs 1207-1212, profiles/r5_kernel_ab/
+    # rows_sched_nonuniform_2e7.txt; round 2: max-memory-clause 0.1255 vs default 0.1265 s
+    # on 1e8, ilp 0.131, iterative-ilp 0.138, profiles/archive/r2_kernel/README.txt)
     # candidates arrive in SGPRs: packed-math pairs would need them moved into VGPRs;
     # iterative-minreg scheduling: 1e8 k=100 74.4 vs 76.8 ms (iterative-maxocc 75.1,
     # max-memory-clause 77.5, max-ilp 78.1, iterative-ilp 77.4; profiles/r5_kernel_ab/sched_1e8.txt)
@@ -77,7 +79,7 @@ FILE_FLAGS = {
     # the f16 fragment packing must stay in the explicit cvt_pkrtz / perm form
     "knn_mfma.hip": ["-fno-slp-vectorize"],
     "knn_rows.hip": ["-fno-slp-vectorize", "-mllvm", "-disable-promote-alloca-to-vector",
-                     "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+                     "-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"],
 }
 
 
