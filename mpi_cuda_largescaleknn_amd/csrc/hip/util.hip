@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void morton_kernel(const float *__restrict__ p
 // has kG3Per random loads in flight — stages it in LDS and writes it out as float4s
 // (fully coalesced, instead of three stride-12 dword stores per row). Partial last tile:
 // direct stores.
-constexpr int kG3Per = 4;
+constexpr int kG3Per = 4;  // 8 / 16 rows per lane: same 26.1-26.7 ms at 1B (profiles/r5_sort/gather_tile_1b.txt)
 constexpr int kG3Tile = 256 * kG3Per;
 
 __global__ __launch_bounds__(256) void gather3_kernel(const float *__restrict__ src,
