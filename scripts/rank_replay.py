@@ -111,9 +111,13 @@ for r in range(P):
     fin = torch.empty(nr, dtype=torch.float32, device=DEV)
 
     def local():
+        # as knn_with_halo: both passes queued back to back, their failure checks deferred
+        pend: list = []
         E.query(index, cfg, hint2, out=d2, final_out=fin, groups=blist, ngroups=ng, ngroups_dev=bcnt,
-                short_list=True)
-        E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng, ngroups_dev=icnt)
+                short_list=True, deferred=pend)
+        E.query(index, cfg, hint2, out=d2, final_out=fin, groups=ilist, ngroups=ng, ngroups_dev=icnt,
+                deferred=pend)
+        E.settle(pend)
 
     _, t_local = timed(local)
     # the two launches apart, and the whole rank in one launch without lists (the kernel's
