@@ -44,3 +44,18 @@ def test_hip_library_builds():
         pytest.skip("hipcc not available")
     path = B.build_hip()
     assert os.path.exists(path)
+
+
+def test_flag_change_rebuilds_hip_objects(monkeypatch):
+    """FILE_FLAGS live in _build.py: the library and every object depend on that file, so a
+    changed compile flag cannot leave an object built with the old flags in the library."""
+    seen = []
+
+    def fake_stale(target, deps):
+        seen.append((os.path.basename(target), list(deps)))
+        return False  # nothing to rebuild: only the dependency lists are checked
+
+    monkeypatch.setattr(B, "_stale", fake_stale)
+    B.build_hip()
+    assert seen and seen[0][0] == os.path.basename(B.HIP_LIB)
+    assert os.path.abspath(B.__file__) in [os.path.abspath(d) for d in seen[0][1]]
