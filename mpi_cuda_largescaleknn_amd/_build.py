@@ -76,8 +76,6 @@ FILE_FLAGS = {
     # iterative-minreg scheduling: 1e8 k=100 74.4 vs 76.8 ms (iterative-maxocc 75.1,
     # max-memory-clause 77.5, max-ilp 78.1, iterative-ilp 77.4; profiles/r5_kernel_ab/sched_1e8.txt)
     "knn_grid.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
-    # the f16 fragment packing must stay in the explicit cvt_pkrtz / perm form
-    "knn_mfma.hip": ["-fno-slp-vectorize"],
     "knn_rows.hip": ["-fno-slp-vectorize", "-mllvm", "-disable-promote-alloca-to-vector",
                      "-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"],
 }

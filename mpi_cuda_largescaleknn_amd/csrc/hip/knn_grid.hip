@@ -24,11 +24,15 @@
 //    every VALU op of the canonical d² takes them as an operand — 6 VALU per candidate and
 //    lane, no broadcast, no per-row queues or logs; the next batch's loads (across segment
 //    boundaries) are issued before the current batch is computed;
-//  * the histogram update is branch-free (LSK_GRID_PAIRHIST): lanes l and l+32 share one
-//    dword per bin row, every candidate adds to its bin or to a per-lane trash row through
-//    a select between two LDS addresses, and the select's compare also counts c_hi —
-//    6 VALU per candidate, no exec-mask round trip. The kernel is VALU-cycle bound: a
-//    wave64 op takes 2 cycles on the 32-lane SIMD, packed f32 ops take 4 (no gain), and an
+//  * the histogram update is branch-free: lanes l and l+32 share one dword per bin row,
+//    and every candidate adds to the row of its value CLAMPED into the lane's range with
+//    one v_med3_u32 — values past the range top land in the row just above the top bin
+//    (the "clamp row"), values below it in bin 0. The count below the top (c_hi) is not
+//    counted per candidate: it is derived once per cell from the wave's add count minus
+//    the clamp row (read and zeroed, "fold"). 3 VALU per candidate (med3, shift,
+//    shift-add) instead of 6 (round 6; round 3's form selected between a bin and a trash
+//    address and counted c_hi with a carry-add). The kernel is VALU-cycle bound: a wave64
+//    op takes 2 cycles on the 32-lane SIMD, packed f32 ops take 4 (no gain), and an
 //    exec-masked half wave costs a full op (profiles/r3_pairs, profiles/r3_hist).
 //
 // Every cull is conservative: cell boxes are the quantisation intervals widened by a
@@ -129,31 +133,58 @@ enum : uint32_t {
 struct Lane {
   float qx, qy, qz;
   uint32_t state;
-  uint32_t lo_b, hi_b, shift;  // histogram range; lo_b holds the answer once DONE
+  // histogram range [lo_b, hi_b) in bins of 2^shift: lo_b is a multiple of 2^shift and
+  // hi_b = lo_b + bin_hi << shift (a whole number of bins; a cutoff is applied to the
+  // result, not to the range). lo_b holds the answer once DONE. hi_b = 0: nothing more
+  // can count (the zero probe's k exact copies).
+  uint32_t lo_b, hi_b, shift;
   int32_t bin_hi;
-  uint32_t c_hi;     // values < hi_b counted this pass (exact, 32-bit)
+  uint32_t c_hi;     // values < hi_b this pass (exact, 32-bit; derived: adds - above)
+  uint32_t above;    // values of this pass at or above the top: folded clamp row + dropped bins
   uint32_t c_base;   // exact count below lo_b, or kUnknown (READY: count below the band)
   uint32_t nudf;
   uint32_t band_lo, band_w, bc;
   uint32_t coff, ccnt;
+  // operands of the histogram add (hist_regs): clamp top, row base, per-lane increment
+  uint32_t chi, hbase, inc;
 };
 
 __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift, uint32_t top_limit,
                                           uint32_t c_base) {
-  s.lo_b = lo_b;
-  s.c_base = lo_b == 0 ? 0u : c_base;
+  // bins start at a multiple of 2^shift (the histogram add then needs no subtraction);
+  // a lower start than asked for loses the exact count below it
+  const uint32_t lo = lo_b & ~((1u << shift) - 1u);
+  s.lo_b = lo;
+  s.c_base = lo == 0 ? 0u : (lo == lo_b ? c_base : kUnknown);
   s.shift = shift;
-  const uint64_t top = (uint64_t)lo_b + ((uint64_t)kBins << shift);
-  const uint64_t hi = top < (uint64_t)top_limit ? top : (uint64_t)top_limit;
-  s.hi_b = (uint32_t)hi;
-  s.bin_hi = hi > lo_b ? (int32_t)((hi - lo_b + ((1ull << shift) - 1)) >> shift) : 0;
+  // the fewest whole bins (<= kBins) that reach top_limit
+  const uint64_t span = top_limit > lo ? (uint64_t)(top_limit - lo) : 0ull;
+  const uint64_t nb = (span + ((1ull << shift) - 1)) >> shift;
+  s.bin_hi = (int32_t)(nb < (uint64_t)kBins ? nb : (uint64_t)kBins);
+  s.hi_b = lo + ((uint32_t)s.bin_hi << shift);
   s.c_hi = 0;
+  s.above = 0;
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 __device__ __forceinline__ uint32_t lds_addr(uint32_t *p) { return (uint32_t)(uintptr_t)(lds_u32 *)p; }
 __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
   __atomic_fetch_add((lds_u32 *)(uintptr_t)addr, v, __ATOMIC_RELAXED);
+}
+// this lane's 16-bit half of a histogram dword (byte address)
+__device__ __forceinline__ uint32_t lds_read16(uint32_t addr) { return *(lds_u16 *)(uintptr_t)addr; }
+__device__ __forceinline__ void lds_zero16(uint32_t addr) { *(lds_u16 *)(uintptr_t)addr = 0; }
+// LDS byte address of the histogram row of v clamped into [lo, hi]: base + ((med3 >> sh) << 7).
+// One asm block: the compiler forms med3 only for constant bounds (else max + min), and a
+// lone asm med3 gets an s_nop before its VALU consumer (it might be a transcendental).
+__device__ __forceinline__ uint32_t hist_row_addr(uint32_t v, uint32_t lo, uint32_t hi, uint32_t sh,
+                                                  uint32_t base) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3\n\tv_lshrrev_b32 %0, %4, %0\n\tv_lshl_add_u32 %0, %0, 7, %5"
+      : "=&v"(r)
+      : "v"(v), "v"(lo), "v"(hi), "v"(sh), "v"(base));
+  return r;
 }
 
 __device__ __forceinline__ uint32_t hist_read(const uint32_t *pool, uint32_t b, int lane) {
@@ -176,18 +207,6 @@ __device__ __forceinline__ void underflow_restart(Lane &s) {
   s.nudf++;
 }
 
-// Drop top bins while at least k counted values stay below: the lane's bound shrinks.
-__device__ __forceinline__ void hist_shrink(Lane &s, const uint32_t *pool, int lane, uint32_t k) {
-  while (s.bin_hi > 0) {
-    const uint32_t top = hist_read(pool, (uint32_t)s.bin_hi - 1u, lane);
-    if (s.c_hi - top < k) break;
-    s.c_hi -= top;
-    s.bin_hi--;
-    s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
-  }
-  // k exact zeros: the k-th is 0 and nothing can be closer (knn_rows zero probe)
-  if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
-}
 
 // 16-bit bin checksum (see knn_rows.hip hist_consistent): the counter sum over [0, bin_hi)
 // equals c_hi iff no counter wrapped.
@@ -260,15 +279,57 @@ struct GridCtx {
                            // xyz), [8r+6] its squared cull radius (cull_r2); read per cell
                            // (in SGPRs they pushed spill reloads into the candidate loop)
   uint32_t *pool;
-  uint32_t trash;          // LDS byte address of this lane's trash-row counter (opaque)
+  uint32_t row0;           // LDS byte address of this lane's dword in histogram row 0
+  uint32_t hoff;           // byte offset of this lane's 16-bit half (lanes l, l+32 share a dword)
+  uint32_t inc;            // this lane's histogram increment: 1 or 1 << 16
   int lane;
   uint32_t k;
+  uint32_t adds;           // histogram adds per lane this pass (wave-uniform)
   uint32_t evals, cells_n, segs;
 #ifdef LSK_GRID_PROFILE
   uint64_t prof[8];
   uint32_t ev_mode[2];
 #endif
 };
+
+// The histogram add's operands after a change of the lane's range or state. A lane that
+// is not histogramming adds 0 (to its row 0).
+__device__ __forceinline__ void hist_regs(Lane &s, const GridCtx &G) {
+  const bool h = s.state == ST_HIST;
+  s.chi = h ? s.lo_b + ((uint32_t)s.bin_hi << s.shift) : s.lo_b;
+  s.hbase = G.row0 - ((s.lo_b >> s.shift) << 7);
+  s.inc = h ? G.inc : 0u;
+}
+
+// Fold the clamp row (row bin_hi: every value at or above the top since the last fold)
+// into `above` and zero it, then c_hi = adds - above. Called once per cell, so the clamp
+// row never holds more than one cell's values (no 16-bit wrap on long passes).
+__device__ __forceinline__ void hist_fold(Lane &s, const GridCtx &G) {
+  if (s.state == ST_HIST) {
+    const uint32_t a = G.row0 + G.hoff + ((uint32_t)s.bin_hi << 7);
+    s.above += lds_read16(a);
+    lds_zero16(a);
+    s.c_hi = G.adds - s.above;
+  }
+}
+
+// Drop top bins while at least k counted values stay below: the lane's bound shrinks. A
+// dropped bin becomes the clamp row (its values move to `above`, the row is zeroed).
+__device__ __forceinline__ void hist_shrink(Lane &s, const GridCtx &G) {
+  const uint32_t k = G.k;
+  while (s.bin_hi > 0) {
+    const uint32_t top = hist_read(G.pool, (uint32_t)s.bin_hi - 1u, G.lane);
+    if (s.c_hi - top < k) break;
+    s.c_hi -= top;
+    s.above += top;
+    s.bin_hi--;
+    lds_zero16(G.row0 + G.hoff + ((uint32_t)s.bin_hi << 7));
+    s.hi_b = s.lo_b + ((uint32_t)s.bin_hi << s.shift);
+  }
+  // k exact zeros: the k-th is 0 and nothing can be closer (knn_rows zero probe)
+  if (s.bin_hi == 1 && s.lo_b == 0u && s.shift == 0u && s.c_hi >= k) s.hi_b = 0u;
+  hist_regs(s, G);
+}
 
 // Cell coordinate at level l (monotone in v: a point with coordinate v' <= v never lies in
 // a later cell — the same float ops as the sort keys, common.h morton_quant).
@@ -327,32 +388,27 @@ __device__ __forceinline__ float cull_r2(const Lane &s, GridCtx &G) {
   return __uint_as_float(max(max(a, b), max(c, d)));
 }
 
+#ifndef LSK_GRID_HSKIP
+#define LSK_GRID_HSKIP 0  // 1: skip a 4-candidate histogram step when no lane has a value below its top (1e8 k=100: 80.3 vs 74.3 ms, profiles/r6_hist)
+#endif
 template <int MODE>
-__device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3,
-                                        uint32_t *pool, int lane, uint32_t hist_trash) {
+__device__ __forceinline__ void update4(Lane &s, GridCtx &G, uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3) {
   if (MODE == MODE_HIST) {
-    const uint32_t um = min(min(u0, u1), min(u2, u3));
-    if (!__ballot(um < s.hi_b)) return;
-    const uint32_t hb = s.hi_b, lb = s.lo_b, sh = s.shift;
+    if (LSK_GRID_HSKIP) {
+      const uint32_t um = min(min(u0, u1), min(u2, u3));
+      if (!__ballot(um < s.hi_b)) return;
+    }
     const uint32_t u[4] = {u0, u1, u2, u3};
-    // every slot adds, without a branch: a value below hi_b to its bin (< bin_hi), any
-    // other (past the range, or a lane not histogramming: hi_b = 0) to the trash row kBins,
-    // which nothing reads; the compare also counts c_hi. A 16-bit wrap (65536 adds to one
-    // bin in a pass) lands in a counter hist_consistent checks, or carries into the
-    // partner lane's same row: a checked counter of its, or one nothing reads.
-    // 6 VALU per candidate (sub_sat, shift, compare, select, address, carry-add) and no
-    // exec-mask round trip: 0.0885 vs 0.0955 s on 1e8 uniform points, k = 100.
-    // (byte addresses: the row address is one shift-add, the trash address an opaque
-    // per-lane value, so the select picks between addresses, not bin indices)
-    const uint32_t inc = 1u << (((uint32_t)lane & 32u) >> 1);
-    const uint32_t row0 = lds_addr(pool) + ((uint32_t)lane & 31u) * 4u, trash = hist_trash;
+    // every slot adds, without a branch or a compare: the value clamped into [lo_b, top]
+    // (v_med3_u32) picks the row — its bin, bin 0 below the range, the clamp row (bin_hi)
+    // at or above the top — and lo_b being a multiple of 2^shift folds the bin offset into
+    // the per-lane row base: med3, shift, shift-add (3 VALU; round 3-5: 6). The count below
+    // the top is derived per cell (hist_fold). A 16-bit wrap (65536 adds to one in-range
+    // bin in a pass) is caught by hist_consistent (the clamp row is zeroed every cell).
+    G.adds += 4u;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-      const uint32_t v = u[t];
-      const bool in = v < hb;
-      const uint32_t a = in ? row0 + ((__builtin_elementwise_sub_sat(v, lb) >> sh) << 7) : trash;
-      lds_add(a, inc);
-      s.c_hi += in ? 1u : 0u;
+      lds_add(hist_row_addr(u[t], s.lo_b, s.chi, s.shift, s.hbase), s.inc);
     }
   } else {
     const uint32_t bl = s.band_lo, bw = s.band_w;
@@ -362,7 +418,7 @@ __device__ __forceinline__ void update4(Lane &s, uint32_t u0, uint32_t u1, uint3
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       if (u[t] - bl < bw) {
-        if (s.ccnt < s.bc) pool[s.coff + s.ccnt] = u[t];
+        if (s.ccnt < s.bc) G.pool[s.coff + s.ccnt] = u[t];
         s.ccnt++;
       }
     }
@@ -389,8 +445,11 @@ constexpr uint32_t kSegCheck = 1024;  // candidates between bound checks in a lo
 
 template <int MODE>
 __device__ __forceinline__ void shrink_all(Lane &s, GridCtx &G) {
-  if (MODE == MODE_HIST && __ballot(s.state == ST_HIST && s.c_hi >= G.k)) {
-    if (s.state == ST_HIST && s.c_hi >= G.k) hist_shrink(s, G.pool, G.lane, G.k);
+  if (MODE == MODE_HIST) {
+    hist_fold(s, G);
+    if (__ballot(s.state == ST_HIST && s.c_hi >= G.k)) {
+      if (s.state == ST_HIST && s.c_hi >= G.k) hist_shrink(s, G);
+    }
   }
 }
 
@@ -400,7 +459,7 @@ __device__ __forceinline__ void eval4(Lane &s, GridCtx &G, const Batch &b) {
   const uint32_t u1 = fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1));
   const uint32_t u2 = fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2));
   const uint32_t u3 = fbits(lsk::dist2(s.qx - b.x3, s.qy - b.y3, s.qz - b.z3));
-  update4<MODE>(s, u0, u1, u2, u3, G.pool, G.lane, G.trash);
+  update4<MODE>(s, G, u0, u1, u2, u3);
 }
 
 // The 64 grandchild slots of one level-lc cell, fetched ahead of use (one 16-byte vector
@@ -430,7 +489,7 @@ __device__ __forceinline__ void eval4_tail(Lane &s, GridCtx &G, const Batch &b, 
   const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
   const uint32_t u1 = left > 1u ? fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1)) : ~0u;
   const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
-  update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane, G.trash);
+  update4<MODE>(s, G, u0, u1, u2, ~0u);
 }
 
 #if LSK_GRID_BATCH == 8
@@ -578,7 +637,7 @@ __device__ __forceinline__ void process_segment(Lane &s, GridCtx &G, uint32_t i0
     const uint32_t u0 = fbits(lsk::dist2(s.qx - b.x0, s.qy - b.y0, s.qz - b.z0));
     const uint32_t u1 = left > 1u ? fbits(lsk::dist2(s.qx - b.x1, s.qy - b.y1, s.qz - b.z1)) : ~0u;
     const uint32_t u2 = left > 2u ? fbits(lsk::dist2(s.qx - b.x2, s.qy - b.y2, s.qz - b.z2)) : ~0u;
-    update4<MODE>(s, u0, u1, u2, ~0u, G.pool, G.lane, G.trash);
+    update4<MODE>(s, G, u0, u1, u2, ~0u);
   }
   G.evals += (i1 - i0 + 3u) & ~3u;  // (an early stop counts the whole segment)
   G.segs++;

@@ -265,19 +265,6 @@ def radius_hint(box: torch.Tensor, n_total: int, k: int) -> torch.Tensor:
 
 
 ROWS_MAX_K = 65535  # 16-bit histogram bins of knn_rows; larger k go to the exact kernel
-# Grid-path kernel: "mfma" (knn_mfma.hip: MFMA-screened 32-query tiles, band lists) for
-# k in [MFMA_MIN_K, MFMA_MAX_K], else "sgpr" (knn_grid.hip: SGPR candidate streams, LDS
-# histogram). The band list of a query holds ~2 z sqrt(k) values: beyond MFMA_MAX_K it
-# would overflow the per-query LDS capacity (knn_mfma.hip kCapQ).
-GRID_KERNEL = os.environ.get("LSKNN_GRID_KERNEL", "sgpr")
-MFMA_MIN_K, MFMA_MAX_K = 2, 128
-
-
-def grid_kernel_for(k: int) -> str:
-    """Which grid-path kernel serves k (GRID_KERNEL, within the mfma kernel's k range)."""
-    return "mfma" if GRID_KERNEL == "mfma" and MFMA_MIN_K <= k <= MFMA_MAX_K else "sgpr"
-
-
 FAIL_CAP_OVERRIDE: int | None = None  # tests: force failure-list overflows (whole reruns)
 
 
@@ -441,10 +428,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
                 a.pad2 = full if expect_grid else 1
             else:
                 a.pad2 = full
-            if grid_kernel_for(k) == "mfma":
-                check(lib.lsk_hip_knn_mfma(C.byref(a), C.byref(gv), st), "knn_mfma")
-            else:
-                check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
+            check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
             if gate is not None:
                 a.gate_on = 0
                 a.pad2 = 1 if expect_grid else full

@@ -63,7 +63,7 @@ for name in os.environ.get("LSK_DISTS", "clustered,planar,uniform").split(","):
         c = st.counters
         chk = V.sampled_exact(SingleComm(dev), pts, out, 0, n, k, 256)
         bad_ref = int((out != ref).sum())
-        print(f"  level {g} ({K.GRID_KERNEL}): k-NN {t_q * 1e3:.1f} ms; evals/q {c.get('evals', 0) / n:.0f} "
+        print(f"  level {g} (grid): k-NN {t_q * 1e3:.1f} ms; evals/q {c.get('evals', 0) / n:.0f} "
               f"passes/wave {c.get('hist_passes', 0) / max(c.get('waves', 1), 1):.2f} "
               f"fallback {c.get('fallback_queries', 0)} fail {c.get('failed_lanes', 0)}; "
               f"oracle {chk['exact']}/{chk['samples']}; vs production {n - bad_ref}/{n} equal", flush=True)
