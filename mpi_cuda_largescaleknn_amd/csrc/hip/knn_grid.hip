@@ -157,9 +157,12 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
   s.lo_b = lo;
   s.c_base = lo == 0 ? 0u : (lo == lo_b ? c_base : kUnknown);
   s.shift = shift;
-  // the fewest whole bins (<= kBins) that reach top_limit
+  // the fewest whole bins (<= kBins) that reach top_limit, ending at or below +inf (a value
+  // at or past the top — +inf padding included — lands in the clamp row)
   const uint64_t span = top_limit > lo ? (uint64_t)(top_limit - lo) : 0ull;
-  const uint64_t nb = (span + ((1ull << shift) - 1)) >> shift;
+  uint64_t nb = (span + ((1ull << shift) - 1)) >> shift;
+  const uint64_t nb_inf = lo < lsk::kInfBits ? (uint64_t)(lsk::kInfBits - lo) >> shift : 0ull;
+  nb = nb < nb_inf ? nb : nb_inf;
   s.bin_hi = (int32_t)(nb < (uint64_t)kBins ? nb : (uint64_t)kBins);
   s.hi_b = lo + ((uint32_t)s.bin_hi << shift);
   s.c_hi = 0;
@@ -286,6 +289,9 @@ struct GridCtx {
   uint32_t k;
   uint32_t adds;           // histogram adds per lane this pass (wave-uniform)
   uint32_t evals, cells_n, segs;
+#ifdef LSK_ROWQ_STATS
+  uint32_t rq_steps, rq_took, rq_refills;
+#endif
 #ifdef LSK_GRID_PROFILE
   uint64_t prof[8];
   uint32_t ev_mode[2];
@@ -698,10 +704,266 @@ constexpr uint32_t kScanAll = 1u << 16;
 template <int MODE>
 __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n);
 
+#ifndef LSK_GRID_ROWQ
+#define LSK_GRID_ROWQ 0
+#endif
+#ifndef LSK_ROWQ_LOW
+#define LSK_ROWQ_LOW 1  // a row with at most this many queued segments asks for the next cell
+#endif
+#if LSK_GRID_ROWQ
+// ------------------------------------------------------------------ per-row candidate streams
+// Each 16-query row streams ITS OWN candidates (round 6; the SGPR form above streams the
+// union of the four rows' needs to all 64 lanes). Cells are still taken nearest first by
+// the wave, tested per row (process_cell's row boxes and radii), and each row's runs of
+// needed grandchildren ("segments") are appended to that row's queue; a step takes the
+// next 16 candidates of every row at once: lane j of row r loads candidate j of its row
+// (one vector load, issued a step ahead) and the row's 16 lanes read it with a DPP
+// row_newbcast folded into the distance's v_subrev_f32_dpp. Rows consume their queues
+// independently across cells, so a row never pays for another row's candidates.
+//
+// Queue of row r: lanes 16r + t of (qa, qe) hold its t-th segment [qa, qe) of the sorted
+// points (t = 0: the head, partly consumed: qa advances); qn = segments queued (the same
+// in every lane of the row). A full queue (16) blocks the next cell; within one cell, the
+// segments past the 16th are merged into the 16th (the slots between them are unneeded by
+// that row and lie in the same cell: extra candidates, never a repeated one).
+template <int J>
+__device__ __forceinline__ float rowb(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + J, 0xf, 0xf, false));
+}
+template <int J>
+__device__ __forceinline__ uint32_t rowb_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + J, 0xf, 0xf, false);
+}
+// lane j of each row <- lane j + 1 (lane 15 <- 0)
+__device__ __forceinline__ uint32_t row_shl1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, true);
+}
+
+struct RowQ {
+  uint32_t qa, qe, qn;
+};
+struct RowPts {
+  float x, y, z;
+};
+
+// The next (up to) 16 candidates of this lane's row: lane j loads candidate j (padding:
+// the +inf point, d² = +inf, at or past every range top and collect band). At most one
+// segment boundary per step; a consumed head segment is popped (the queue shifts down).
+__device__ __forceinline__ RowPts rowq_take(RowQ &Q, GridCtx &G) {
+  const uint32_t j = (uint32_t)G.lane & 15u;
+  const uint32_t a0 = rowb_u<0>(Q.qa), e0 = rowb_u<0>(Q.qe), a1 = rowb_u<1>(Q.qa), e1 = rowb_u<1>(Q.qe);
+  const uint32_t l0 = e0 - a0, l1 = e1 - a1;
+  const uint32_t took = min(l0 + l1, 16u);
+#ifdef LSK_ROWQ_STATS
+  G.rq_steps++;
+  G.rq_took += (uint32_t)__builtin_amdgcn_readlane((int)took, 0) + (uint32_t)__builtin_amdgcn_readlane((int)took, 16) +
+               (uint32_t)__builtin_amdgcn_readlane((int)took, 32) + (uint32_t)__builtin_amdgcn_readlane((int)took, 48);
+#endif
+  const uint32_t idx = j < l0 ? a0 + j : a1 + (j - l0);
+  const float *p = j < took ? G.pts + 3ull * idx : G.inf4;
+  const RowPts r{p[0], p[1], p[2]};
+  const bool pop = took >= l0 && Q.qn > 0u;
+  const uint32_t sa = row_shl1(Q.qa), se = row_shl1(Q.qe);
+  Q.qa = pop ? sa : Q.qa;
+  Q.qe = pop ? se : Q.qe;
+  if (j == 0u) Q.qa = pop ? a1 + (took - l0) : a0 + took;
+  Q.qn -= pop ? 1u : 0u;
+  return r;
+}
+
+template <int J>
+__device__ __forceinline__ uint32_t rcand(const Lane &s, const RowPts &p) {
+  return fbits(lsk::dist2(s.qx - rowb<J>(p.x), s.qy - rowb<J>(p.y), s.qz - rowb<J>(p.z)));
+}
+
+template <int MODE>
+__device__ __forceinline__ void rowq_eval(Lane &s, GridCtx &G, const RowPts &p) {
+  update4<MODE>(s, G, rcand<0>(s, p), rcand<1>(s, p), rcand<2>(s, p), rcand<3>(s, p));
+  update4<MODE>(s, G, rcand<4>(s, p), rcand<5>(s, p), rcand<6>(s, p), rcand<7>(s, p));
+  update4<MODE>(s, G, rcand<8>(s, p), rcand<9>(s, p), rcand<10>(s, p), rcand<11>(s, p));
+  update4<MODE>(s, G, rcand<12>(s, p), rcand<13>(s, p), rcand<14>(s, p), rcand<15>(s, p));
+  G.evals += 16u;
+#ifdef LSK_GRID_PROFILE
+  G.ev_mode[MODE] += 16u;
+#endif
+}
+
+// One level-lc cell: every row's segments are appended to its queue.
+__device__ __forceinline__ void cell_rows(GridCtx &G, const CellLoad &c, RowQ &Q) {
+  const bool ne = c.e > c.a;
+  const uint64_t nonempty = __ballot(ne);
+  if (!nonempty) return;
+  G.cells_n++;
+  const uint32_t sh = 10u - (G.lc + 2u);
+  const uint32_t last = (1023u >> sh);
+  float lx, hx, ly, hy, lz, hz;
+  cell_span(G, G.ox, c.xyz & 1023u, sh, last, lx, hx);
+  cell_span(G, G.oy, (c.xyz >> 10) & 1023u, sh, last, ly, hy);
+  cell_span(G, G.oz, c.xyz >> 20, sh, last, lz, hz);
+  uint64_t need[kCullGroups];
+#pragma unroll
+  for (int r = 0; r < kCullGroups; r++) {
+    const float *b = G.rbox + 8 * r;
+    const float g2 = lsk::dist2(gap1(lx, hx, b[0], b[3]), gap1(ly, hy, b[1], b[4]), gap1(lz, hz, b[2], b[5]));
+    need[r] = __ballot(ne && g2 <= b[6]);
+  }
+  uint32_t qa = Q.qa, qe = Q.qe, qn = Q.qn;
+#pragma unroll
+  for (int r = 0; r < kCullGroups; r++) {
+    uint64_t nd = need[r];
+    if (!nd) continue;
+    const uint64_t fr = nd | ~nonempty;  // runs of needed or empty slots are contiguous in memory
+    uint32_t t = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)qn, 16 * r));
+    do {
+      const uint32_t t0 = (uint32_t)__builtin_ctzll(nd);
+      const uint64_t after = ~fr >> t0;
+      const uint32_t len = after ? (uint32_t)__builtin_ctzll(after) : 64u - t0;
+      const uint64_t run = (len >= 64u ? ~0ull : ((1ull << len) - 1ull)) << t0;
+      const uint32_t t1 = 63u - (uint32_t)__builtin_clzll(nd & run);
+      nd &= ~run;
+      const uint32_t a = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)c.a, (int)t0));
+      const uint32_t e = lsk::uniform((uint32_t)__builtin_amdgcn_readlane((int)c.e, (int)t1));
+      // lane 16r + t takes the segment; past 16 entries lane 16r + 15 extends its end
+      const bool at = (uint32_t)G.lane == 16u * r + min(t, 15u);
+      qa = at && t < 16u ? a : qa;
+      qe = at ? e : qe;
+      t += t < 16u ? 1u : 0u;
+      G.segs++;
+    } while (nd);
+    qn = ((uint32_t)G.lane >> 4) == (uint32_t)r ? t : qn;
+  }
+  Q.qa = qa;
+  Q.qe = qe;
+  Q.qn = qn;
+}
+
+// One pass with per-row streams. The cells in range are visited in chunks of at most
+// 16 x 16 x (256 / 256..) cells (one chunk for a normal range), nearest first inside a
+// chunk: lane l holds chunk cells l, l+64, l+128, l+192 with their gap to the wave box.
+// A range of more than kMaxCells cells is one segment of all points per row (n <= kScanAll)
+// or the backstop (returns false).
+template <int MODE>
+__device__ __forceinline__ bool grid_pass_rows(Lane &s, GridCtx &G, uint32_t n) {
+  float r2 = cull_r2<MODE>(s, G);
+  if (fbits(r2) == 0u) return true;
+  const uint32_t sh = 10u - G.lc;
+  const float r = sqrtf(r2);
+  const uint32_t x0 = cell_of(G.wlx - r, G.ox, G.scale, sh), x1 = cell_of(G.whx + r, G.ox, G.scale, sh);
+  const uint32_t y0 = cell_of(G.wly - r, G.oy, G.scale, sh), y1 = cell_of(G.why + r, G.oy, G.scale, sh);
+  const uint32_t z0 = cell_of(G.wlz - r, G.oz, G.scale, sh), z1 = cell_of(G.whz + r, G.oz, G.scale, sh);
+  const uint32_t nx = x1 - x0 + 1u, ny = y1 - y0 + 1u, nz = z1 - z0 + 1u;
+  const bool scan_all = (uint64_t)nx * ny * nz > kMaxCells;
+  if (scan_all && n > kScanAll) return false;
+  const uint32_t cxn = min(nx, 16u), cyn = min(ny, 16u), czn = max(1u, min(nz, 256u / (cxn * cyn)));
+  const uint32_t ncx = (nx + cxn - 1u) / cxn, ncy = (ny + cyn - 1u) / cyn, ncz = (nz + czn - 1u) / czn;
+  const uint32_t nchunks = scan_all ? 0u : ncx * ncy * ncz;
+  uint32_t chunk = 0, bx = 0, by = 0, bz = 0, tx = 1, ty = 1, tot = 0, inx = 0, iny = 0;
+  const uint32_t l = (uint32_t)G.lane;
+  float g0 = __builtin_inff(), g1 = g0, g2 = g0, g3 = g0;
+  // chunk k: its origin and size (clipped at the range end) and the gaps of its cells
+  auto load_chunk = [&](uint32_t k) {
+    const uint32_t kx = k % ncx, ky = (k / ncx) % ncy, kz = k / (ncx * ncy);
+    bx = x0 + kx * cxn;
+    by = y0 + ky * cyn;
+    bz = z0 + kz * czn;
+    tx = min(cxn, x1 + 1u - bx);
+    ty = min(cyn, y1 + 1u - by);
+    const uint32_t tz = min(czn, z1 + 1u - bz);
+    tot = tx * ty * tz;
+    inx = (65536u + tx - 1u) / tx;  // exact for c < 256
+    iny = (65536u + ty - 1u) / ty;
+    auto gap_of = [&](uint32_t c) {
+      const uint32_t q = (c * inx) >> 16, rr = (q * iny) >> 16;
+      return c < tot ? cell_gap2(G, bx + c - q * tx, by + q - rr * ty, bz + rr, sh) : __builtin_inff();
+    };
+    g0 = gap_of(l);
+    g1 = tot > 64u ? gap_of(l + 64u) : __builtin_inff();
+    g2 = tot > 128u ? gap_of(l + 128u) : __builtin_inff();
+    g3 = tot > 192u ? gap_of(l + 192u) : __builtin_inff();
+  };
+  if (nchunks) load_chunk(0);
+  CellLoad pend{0u, 0u, 0u};
+  // the nearest cell still within the radius (next chunks when one is exhausted): its
+  // slots are fetched into pend
+  auto next_cell = [&]() -> bool {
+    for (;;) {
+      const float m = wave_min_nonneg(fminf(fminf(g0, g1), fminf(g2, g3)));
+      if (m <= r2) {
+        const uint64_t b0 = __ballot(g0 == m), b1 = __ballot(g1 == m), b2 = __ballot(g2 == m);
+        const uint32_t c = b0 ? (uint32_t)__builtin_ctzll(b0)
+                              : b1 ? 64u + (uint32_t)__builtin_ctzll(b1)
+                                   : b2 ? 128u + (uint32_t)__builtin_ctzll(b2)
+                                        : 192u + (uint32_t)__builtin_ctzll(__ballot(g3 == m));
+        if (l == (c & 63u)) {
+          const uint32_t slot = c >> 6;
+          g0 = slot == 0u ? __builtin_inff() : g0;
+          g1 = slot == 1u ? __builtin_inff() : g1;
+          g2 = slot == 2u ? __builtin_inff() : g2;
+          g3 = slot == 3u ? __builtin_inff() : g3;
+        }
+        const uint32_t q = (c * inx) >> 16, rr = (q * iny) >> 16;
+        pend = fetch_cell(G, bx + c - q * tx, by + q - rr * ty, bz + rr);
+        return true;
+      }
+      if (++chunk >= nchunks) return false;
+      load_chunk(chunk);
+    }
+  };
+  RowQ Q{0u, 0u, 0u};
+  bool have = false;
+  if (scan_all) {
+    // every row streams all points
+    Q.qe = (l & 15u) == 0u ? n : 0u;
+    Q.qn = 1u;
+  } else {
+    have = next_cell();
+    if (!have) return true;
+  }
+
+  // cells while a row runs low and no row's queue is full (the radius is re-read first)
+  auto refill = [&]() {
+    while (have && !__ballot(Q.qn >= 16u) && __ballot(Q.qn <= (uint32_t)LSK_ROWQ_LOW)) {
+      if (MODE == MODE_HIST) r2 = cull_r2<MODE>(s, G);
+#ifdef LSK_ROWQ_STATS
+      G.rq_refills++;
+#endif
+      cell_rows(G, pend, Q);
+      have = fbits(r2) != 0u && next_cell();
+    }
+    return __ballot(Q.qn > 0u) != 0ull;
+  };
+  if (!refill()) return true;
+  RowPts A = rowq_take(Q, G);
+  for (;;) {
+    bool more = refill();
+    RowPts B = rowq_take(Q, G);
+    rowq_eval<MODE>(s, G, A);
+    if (MODE == MODE_HIST) {
+      shrink_all<MODE>(s, G);
+      if (!__ballot(s.state == ST_HIST && s.hi_b > 0u)) break;
+    }
+    if (!more) break;
+    more = refill();
+    A = rowq_take(Q, G);
+    rowq_eval<MODE>(s, G, B);
+    if (MODE == MODE_HIST) {
+      shrink_all<MODE>(s, G);
+      if (!__ballot(s.state == ST_HIST && s.hi_b > 0u)) break;
+    }
+    if (!more) break;
+  }
+  return true;
+}
+#endif
+
 template <int MODE>
 __device__ __forceinline__ bool grid_pass(Lane &s, GridCtx &G, uint32_t n) {
   LSK_GT(tw0);
+#if LSK_GRID_ROWQ
+  const bool ok = grid_pass_rows<MODE>(s, G, n);
+#else
   const bool ok = grid_pass_impl<MODE>(s, G, n);
+#endif
   LSK_GADD(G.prof[2 + MODE], tw0);
   return ok;
 }

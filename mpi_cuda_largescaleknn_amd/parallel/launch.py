@@ -175,30 +175,19 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
             from .rccl import RcclComm
             dist.init_process_group("gloo", rank=rank, world_size=size, timeout=timeout)
             store = dist.distributed_c10d._get_default_store()
-            try:
-                comm, err = RcclComm(device, rank, size, store, force=force_distributed), None
-            except Exception as e:  # noqa: BLE001 (decided together below)
-                comm, err = None, e
-            if chosen is None:
-                # the default, not the user's choice: if any rank could not bring the native
-                # communicator up, every rank falls back to torch's group (agreed over gloo)
-                ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-                if int(ok.item()) == 0:
-                    if comm is not None:
-                        comm.destroy(abort=True)
-                    if rank == 0:
-                        print(f"lsknn: native RCCL communicator unavailable ({err or 'on another rank'}); "
-                              "using torch's process group", flush=True)
-                    opts = dist.ProcessGroupNCCL.Options()
-                    opts.is_high_priority_stream = True
-                    group = dist.new_group(backend="nccl", pg_options=opts)
-                    comm = TorchComm(device, group=group, force=force_distributed)
-                    watchdog = F.Watchdog(rank, size, store).start()
-                    return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
-            elif comm is None:
-                raise err
-            watchdog = F.Watchdog(rank, size, store, comm_check=comm.async_error, on_abort=comm.abort).start()
+
+            def torch_group() -> Comm:
+                if rank == 0:
+                    print("lsknn: native RCCL communicator unavailable on some rank; using torch's process group",
+                          flush=True)
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                group = dist.new_group(backend="nccl", pg_options=opts)
+                return TorchComm(device, group=group, force=force_distributed)
+
+            comm, watchdog = bring_up_native(
+                lambda: RcclComm(device, rank, size, store, force=force_distributed, connect=False),
+                rank, size, store, fallback=None if chosen else torch_group)
             return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
         if backend == "nccl":
             if not use_gpu:
@@ -218,6 +207,47 @@ def init(device_pref: str = "auto", gpu_affinity: int = 0, verbose: bool = False
     else:
         comm = SingleComm(device)
     return Launch(rank, size, local, device, F.MonitoredComm(comm, fault), store, watchdog)
+
+
+def bring_up_native(make, rank: int, size: int, store, fallback=None):
+    """Bring up a native communicator whose init is a blocking collective (RCCL's
+    ncclCommInitRank) without hanging when some rank cannot.
+
+    1. `make()` runs the local steps only (load the library; rank 0 publishes the unique
+       id): a failure there is caught;
+    2. the ranks agree over the gloo control group (MIN of the local results) BEFORE any
+       of them enters the blocking init: if some rank failed, none enters it, and every
+       rank takes `fallback()` (or, with no fallback — the backend was the user's choice —
+       re-raises the local error, or reports the failing peer);
+    3. the watchdog starts, then `connect()`: a rank that fails inside the init publishes
+       the abort key, so the peers' watchdogs end them instead of leaving them blocked.
+    Returns (comm, watchdog). (one non-zero rank failing, or rank 0
+    failing before it published the id, used to leave the others blocked.)"""
+    comm, err = None, None
+    try:
+        comm = make()
+    except Exception as e:  # noqa: BLE001 (decided together below)
+        err = e
+    ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        if fallback is not None:
+            comm = fallback()
+            return comm, F.Watchdog(rank, size, store).start()
+        if err is not None:
+            raise err
+        raise RuntimeError("the native communicator could not be set up on another rank")
+    watchdog = F.Watchdog(rank, size, store).start()
+    try:
+        comm.connect()
+    except Exception as e:
+        try:
+            store.set(F.ABORT_KEY, f"rank {rank}: communicator init failed: {e}")
+        except Exception:  # noqa: BLE001 - raising anyway
+            pass
+        raise
+    watchdog.comm_check, watchdog.on_abort = comm.async_error, comm.abort
+    return comm, watchdog
 
 
 def launcher_env() -> bool:

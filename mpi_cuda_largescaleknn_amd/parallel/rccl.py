@@ -63,7 +63,10 @@ class RcclComm(Comm):
     """One rank of a native RCCL communicator (GPU tensors only)."""
 
     def __init__(self, device: torch.device | str, rank: int, size: int, store, force: bool = False,
-                 key: str = "lsknn/rccl_id", lib_path: str | None = None):
+                 key: str = "lsknn/rccl_id", lib_path: str | None = None, connect: bool = True):
+        """`connect=False`: only the local steps (load RCCL, its version; rank 0 creates and
+        publishes the unique id); `connect()` then runs the blocking ncclCommInitRank, after
+        the ranks agreed that every one of them got this far (launch.bring_up_native)."""
         self._device = torch.device(device)
         if self._device.type != "cuda":
             raise ValueError("RcclComm needs a GPU device")
@@ -77,14 +80,20 @@ class RcclComm(Comm):
         v = C.c_int(0)
         _check(lib.lsk_comm_version(C.byref(v)), "ncclGetVersion")
         self.version = v.value
-        nid = lib.lsk_comm_id_bytes()
+        self._store, self._key, self._h = store, key, None
         if self.rank == 0:
+            nid = lib.lsk_comm_id_bytes()
             buf = C.create_string_buffer(nid)
             _check(lib.lsk_comm_unique_id(buf, nid), "ncclGetUniqueId")
             store.set(key, buf.raw)
-            uid = buf.raw
-        else:
-            uid = bytes(store.get(key))  # blocks until rank 0 published it
+        if connect:
+            self.connect()
+
+    def connect(self) -> None:
+        """ncclCommInitRank (a collective: blocks until every rank has called it)."""
+        lib = _native.comm()
+        nid = lib.lsk_comm_id_bytes()
+        uid = bytes(self._store.get(self._key))  # rank 0 published it before any rank gets here
         if len(uid) != nid:
             raise RuntimeError("RCCL unique id of the wrong size in the store")
         h = C.c_void_p()

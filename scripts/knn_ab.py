@@ -59,6 +59,10 @@ for npts in a.points:
               f"hist adds/w={c.get('collect_nodes', 0) / w:.0f} passes={c.get('hist_passes', 0) / w:.3f} ovf={c.get('overflow_lanes', 0)} "
               f"low={c.get('underflow_lanes', 0)} refine={c.get('refine_lanes', 0)} "
               f"fail={c.get('failed_lanes', 0)} fallback={c.get('fallback_queries', 0)} sha={h}", flush=True)
+        if c.get("prof_rows_entry"):  # LSK_ROWQ_STATS build
+            print(f"  row streams: steps/w {c['prof_rows_entry'] / w:.1f}  real candidates per row "
+                  f"{c['prof_rows_in'] / w / 4:.0f} of {16 * c['prof_rows_entry'] / w:.0f} slots  "
+                  f"refills/w {c.get('list_invalid_waves', 0) / w:.1f}", flush=True)
         if c.get("prof_wave"):
             tot = c["prof_wave"]
             names = ["proc_hist", "proc_collect", "walk_hist", "walk_collect", "quarters", "inner_nodes", "select"]
