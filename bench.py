@@ -61,6 +61,7 @@ from mpi_cuda_largescaleknn_amd.models import knn_engine as E  # noqa: E402
 from mpi_cuda_largescaleknn_amd.models.knn_engine import KnnConfig  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import pipelines as PL  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import refalgo as RA  # noqa: E402
+from mpi_cuda_largescaleknn_amd.parallel import faults as FA  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel import launch as LA  # noqa: E402
 from mpi_cuda_largescaleknn_amd.parallel.stream import SetStream  # noqa: E402
 from mpi_cuda_largescaleknn_amd.utils import trace, verify  # noqa: E402
@@ -234,7 +235,8 @@ def main():
     # eager launches of the stream: 1e6 k=8 711 vs 702 Mpts/s, profiles/archive/r2_s3_table)
     pipelined = (args.pipeline == 1 or (args.pipeline < 0 and n_total >= PIPELINE_MIN_POINTS)) \
         and device.type == "cuda" and args.mode == "halo"
-    host_sets = [make_points(n_total, rank, world, device, args.variant, d) for d in range(2 if pipelined else 1)]
+    with FA.HEARTBEAT.host_phase("make_points"):
+        host_sets = [make_points(n_total, rank, world, device, args.variant, d) for d in range(2 if pipelined else 1)]
     host_outs = [torch.empty(h.shape[0], dtype=torch.float32, pin_memory=device.type == "cuda") for h in host_sets]
     host_pts, host_out = host_sets[0], host_outs[0]
 
@@ -377,6 +379,7 @@ def main():
         # counts every sampled id's distances over all ranks' points)
         b, _ = block_range(n_total, rank, world)
         for d in written:
+            FA.HEARTBEAT.beat("sampled_exact")
             c = verify.sampled_exact(comm, host_sets[d], host_outs[d], b, n_total, args.k, args.verify)
             check = c if check is None else {"samples": check["samples"] + c["samples"],
                                              "exact": check["exact"] + c["exact"],

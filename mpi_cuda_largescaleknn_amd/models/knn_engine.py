@@ -146,8 +146,8 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
                 keys: tuple | None = None, grid: bool = False, density_n: int | None = None,
                 grid_level: int | None = None) -> LocalIndex:
     """Sort points along the space-filling curve of `box` (default: their own bounds) and
-    build the bucket tree. `keys` = (keys, iota) computed already (the streamed upload
-    keys each chunk as it lands). `grid`: also index the sorted points by the cell grid of
+    build the bucket tree. `keys` = (keys, iota) computed already (SetStream's PRE_KEYS:
+    the next set's box and curve keys on the side stream beside the current k-NN). `grid`: also index the sorted points by the cell grid of
     the fast local k-NN pass (build_grid, GPU). `density_n`: the number of points that
     fill `box` (a rank's share of a global box: the global count; default: n).
     `grid_level` (tests): force the grid's grandchild level.
@@ -284,6 +284,13 @@ class host_sync_free:
     def __exit__(self, *exc):
         _SYNC_FREE[0] -= 1
         return False
+
+
+def new_heavy_stream() -> None:
+    """A new stream of sets starts knowing nothing about over-full cells: its first set
+    takes the eager check (SetStream.run). The DEFERRED_HEAVY report is kept."""
+    _HEAVY_PENDING.clear()
+    _HEAVY_KNOWN[0] = None
 
 
 def deferred_heavy_cells(clear: bool = False) -> bool:

@@ -48,6 +48,27 @@ class Heartbeat:
     def __init__(self):
         self.t = time.monotonic()
         self.what = "start"
+        self.host = 0  # > 0: inside a long local host phase (host_phase), not idle
+
+    def host_phase(self, what: str):
+        """Context for a long local phase with no collective (data generation, the sampled
+        check, a library build): the progress timeout does not run inside it, and the
+        heartbeat is beaten on the way in and out (a 150 s bench timeout must
+        only catch time spent waiting on peers)."""
+        hb = self
+
+        class _Phase:
+            def __enter__(self):
+                hb.host += 1
+                hb.beat(what)
+                return self
+
+            def __exit__(self, *exc):
+                hb.host -= 1
+                hb.beat()
+                return False
+
+        return _Phase()
 
     def beat(self, what: str = "") -> None:
         self.t = time.monotonic()
@@ -205,6 +226,8 @@ class Watchdog:
                             pass
                     self._die(f"aborting: {err}", EXIT_COMM_ERROR)
             idle = time.monotonic() - HEARTBEAT.t
+            if HEARTBEAT.host > 0:
+                continue
             if idle > self.timeout and not self._stop.is_set():
                 if self.store is not None:
                     try:

@@ -145,6 +145,7 @@ class SetStream:
         new_info = info_factory or (lambda: PL.RunInfo(PL.PhaseTimer(False, self.device)))
         done = on_done or (lambda i: None)
         if self.gpu:
+            E.new_heavy_stream()  # an earlier stream's clean verdict says nothing about this one
             with E.host_sync_free():  # no host read inside a build (knn_engine.build_index)
                 if self.comm.distributed and self.variant == "prepartitioned":
                     return self._run_prepartitioned(inputs, outputs, new_info, done)

@@ -117,6 +117,29 @@ def test_watchdog_aborts_on_communicator_error(tmp_path):
     assert flag.exists()
 
 
+def test_watchdog_skips_long_host_phase():
+    """a long local host phase (data generation, a library build) is not a hang:
+    inside HEARTBEAT.host_phase the progress timeout does not run; after it, idle time
+    counts again and the rank exits with EXIT_TIMEOUT naming the last op."""
+    import subprocess
+    import sys
+
+    code = (
+        "import time\n"
+        "from mpi_cuda_largescaleknn_amd.parallel import faults as F\n"
+        "F.Watchdog(0, 2, None, timeout=0.5, poll=0.05).start()\n"
+        "with F.HEARTBEAT.host_phase('make_points'):\n"
+        "    time.sleep(2.0)\n"
+        "print('phase done', flush=True)\n"
+        "F.HEARTBEAT.beat('alltoallv')\n"
+        "time.sleep(30)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=root)
+    assert "phase done" in out.stdout, out.stderr
+    assert out.returncode == F.EXIT_TIMEOUT, (out.returncode, out.stderr)
+    assert "timeout in alltoallv" in out.stderr
+
+
 def test_bench_hang_names_the_collective():
     """bench.py's own progress timeout (bench.BENCH_TIMEOUT_S = 150 s, well under the
     driver's 600 s; shortened here through LSKNN_TIMEOUT): a rank hung in a collective

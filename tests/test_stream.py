@@ -282,3 +282,43 @@ def test_stream_clean_sets_stay_sync_free_gpu():
     assert not E.deferred_heavy_cells(clear=True)
     for s, o in zip(S, outs):
         assert torch.equal(o, oracle(s, k))
+
+
+@pytest.mark.gpu
+def test_stream_after_clean_stream_checks_heavy_again_gpu():
+    """a clean stream, then a stream with over-full cells in the same process.
+    The second stream must not inherit the first one's clean verdict: its first set takes
+    the eager check and refines, nothing is left unrefined, outputs exact."""
+    dev = torch.device("cuda", 0)
+    k = 16
+    clean = [GENERATORS["uniform"](50_000, seed=s) for s in (1, 2)]
+    E.deferred_heavy_cells(clear=True)
+    SetStream(SingleComm(dev), E.KnnConfig(k=k)).run([s.pin_memory() for s in clean],
+                                                     [torch.empty(s.shape[0]).pin_memory() for s in clean])
+    assert E._HEAVY_KNOWN[0] is False or E._HEAVY_PENDING  # the clean verdict is known / pending
+    heavy = [GENERATORS["mixed_scale"](60_000, seed=s) for s in (4, 5)]
+    outs = [torch.empty(s.shape[0], dtype=torch.float32).pin_memory() for s in heavy]
+    E.LAST_REFINED = False
+    old = E.HEAVY_RUN
+    E.HEAVY_RUN = 512
+    try:
+        SetStream(SingleComm(dev), E.KnnConfig(k=k)).run([s.pin_memory() for s in heavy], outs)
+    finally:
+        E.HEAVY_RUN = old
+    assert E.LAST_REFINED
+    assert not E.deferred_heavy_cells(clear=True)
+    for s, o in zip(heavy, outs):
+        assert torch.equal(o, oracle(s, k))
+
+
+def test_new_stream_forgets_heavy_verdict_cpu():
+    """SetStream.run resets what an earlier stream learned about over-full cells (but not
+    the DEFERRED_HEAVY report)."""
+    E.deferred_heavy_cells(clear=True)
+    E._HEAVY_KNOWN[0] = False
+    E._HEAVY_PENDING.append(("flag", "event"))
+    E.DEFERRED_HEAVY.append(torch.tensor(False))
+    E.new_heavy_stream()
+    assert E._HEAVY_KNOWN[0] is None and not E._HEAVY_PENDING
+    assert len(E.DEFERRED_HEAVY) == 1
+    E.deferred_heavy_cells(clear=True)
