@@ -66,7 +66,10 @@ using lsk::fbits;
 #endif
 constexpr int kWPB = LSK_GRID_WPB;
 constexpr int kThreads = kWPB * lsk::kWave;
-constexpr int kBins = 40;                 // 16-bit bins
+#ifndef LSK_GRID_BINS
+#define LSK_GRID_BINS 40
+#endif
+constexpr int kBins = LSK_GRID_BINS;      // 16-bit bins
 // Lanes l and l+32 share a dword (low / high half) of each bin row, so a lane's increment
 // is a per-lane constant and every candidate adds without a branch (values past the range
 // go to a trash row, kBins).
@@ -95,17 +98,42 @@ __device__ __forceinline__ float group_min(float v) { return -group_max(-v); }
 // band selection: a bitonic network over up to kNet band values in registers (1e8, k=100:
 // 0.082 -> 0.079 s against the LDS heap for every band; 16 values: no gain, bands of
 // 17..32 then take the heap and the wave runs both)
-constexpr int kNet = 32;
-constexpr int kNetMin = 8;  // the network serves a wave only if some band holds more values
-#ifndef LSK_GRID_TOPBINS
-#define LSK_GRID_TOPBINS 10
+#ifndef LSK_GRID_NET
+#define LSK_GRID_NET 16  // (round 6, with first_range's finer bins; rounds 3-5: 32)
 #endif
-// first range tops out 1.25 octaves of d² above the estimate (1e8 uniform, k=100, nearest-
-// first cells: 8 bins 0.1207 s with 82K overflow lanes, 10 bins 0.1181 s / 6.8K, 12 bins
-// 0.1197 s / 623)
-constexpr int kTopBins = LSK_GRID_TOPBINS;
+#ifndef LSK_GRID_NETMIN
+#define LSK_GRID_NETMIN 4
+#endif
+constexpr int kNet = LSK_GRID_NET;
+constexpr int kNetMin = LSK_GRID_NETMIN;  // the network serves a wave only if some band holds more values
+#ifndef LSK_GRID_ABL
+#define LSK_GRID_ABL 0  // tuning ablations (wrong results): 1 no wrap check, 2 no band network
+#endif
+#ifndef LSK_GRID_TOPBINS
+#define LSK_GRID_TOPBINS 0  // 0: by k (first_range); else fixed (tuning)
+#endif
 constexpr uint32_t kLogBins = 5;          // floor(log2(kBins))
-constexpr uint32_t kShift0 = 20;          // 1/8 octave of d² per bin
+#ifndef LSK_GRID_SHIFT0
+#define LSK_GRID_SHIFT0 0  // 0: by k (first_range); else fixed (tuning)
+#endif
+// First-range resolution and top by k (round 6). The k-th's d² spreads ~2/(3 sqrt k)
+// around the density estimate (6.7 % at k = 100), so the bins of the first range (and of
+// every restart) narrow as k grows: bins of 2^shift0 float ulps (20: 1/8 octave of d², 19:
+// 1/16, 18: 1/32) and a top kTop bins above the estimate. Finer bins make the final band
+// (the k-th's bin) narrower: fewer values to collect and select (16-value network instead
+// of 32) and a smaller collect radius; a lower top makes the first cells cull harder. 1e8
+// uniform, k = 100, bit-identical outputs (profiles/r6_bins): 20 / +10 bins (rounds 3-5)
+// 74.9 ms, 19 / +14 72.6, 18 / +22 70.5; 1B: 773.6 -> 730.3 ms; k in {8..128} at 1e8 in
+// profiles/r6_bins/k_sweep_1e8.txt.
+struct FirstRange {
+  uint32_t shift, top;
+};
+__device__ __forceinline__ FirstRange first_range(uint32_t k) {
+  if (LSK_GRID_SHIFT0 != 0) return FirstRange{(uint32_t)LSK_GRID_SHIFT0, (uint32_t)LSK_GRID_TOPBINS};
+  if (k >= 96u) return FirstRange{18u, 22u};  // (k = 64: 19 / +14 65.4 ms, 18 / +22 66.1)
+  if (k >= 12u) return FirstRange{19u, 14u};  // (k = 8: 19 / +14 38.9 ms, 20 / +10 36.6)
+  return FirstRange{20u, 10u};
+}
 constexpr uint32_t kMaxPasses = 24;
 constexpr uint32_t kUnknown = 0xffffffffu;
 constexpr uint32_t kNaNBits = 0x7fc00000u;
@@ -198,10 +226,10 @@ __device__ __forceinline__ uint32_t top_count(const Lane &s, const uint32_t *poo
   return s.bin_hi > 0 ? hist_read(pool, (uint32_t)s.bin_hi - 1u, lane) : s.c_hi;
 }
 
-__device__ __forceinline__ void underflow_restart(Lane &s) {
+__device__ __forceinline__ void underflow_restart(Lane &s, uint32_t shift0) {
   const uint32_t topb = s.hi_b;
-  if (s.nudf == 0 && topb > ((uint32_t)kBins << kShift0)) {
-    set_range(s, topb - ((uint32_t)kBins << kShift0), kShift0, topb, kUnknown);
+  if (s.nudf == 0 && topb > ((uint32_t)kBins << shift0)) {
+    set_range(s, topb - ((uint32_t)kBins << shift0), shift0, topb, kUnknown);
   } else {
     uint32_t sh = 0;
     while (((uint64_t)kBins << sh) < (uint64_t)topb) sh++;
