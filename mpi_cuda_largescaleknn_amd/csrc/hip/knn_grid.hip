@@ -197,6 +197,20 @@ __device__ __forceinline__ void set_range(Lane &s, uint32_t lo_b, uint32_t shift
   s.above = 0;
 }
 
+// A range that starts at an estimate: if the cutoff lies at or below its (aligned) start,
+// the range would be empty (bin_hi = 0) and a value below the start — the query's own
+// zero at k = 1 — would land in the clamp row, uncounted; such a range starts at 0 instead
+// with bins wide enough that kBins of them reach the cutoff (everything counts below it).
+__device__ __forceinline__ void start_range(Lane &s, uint32_t lo_b, uint32_t shift, uint32_t top_limit) {
+  if ((lo_b & ~((1u << shift) - 1u)) < top_limit) {
+    set_range(s, lo_b, shift, top_limit, kUnknown);
+    return;
+  }
+  uint32_t sh = 0;
+  while (((uint64_t)kBins << sh) < (uint64_t)top_limit) sh++;
+  set_range(s, 0u, sh, top_limit, 0u);
+}
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 __device__ __forceinline__ uint32_t lds_addr(uint32_t *p) { return (uint32_t)(uintptr_t)(lds_u32 *)p; }

@@ -81,6 +81,17 @@ def test_grid_knn_cutoff(k):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("k", [1, 2, 16, 100])
+def test_grid_knn_cutoff_below_first_range(k):
+    """A cutoff at or below the start of the first range (round 6: with the clamped
+    histogram add, an empty range left the query's own zero uncounted at k = 1 and the
+    cutoff came back instead): the range then starts at 0; 0, tiny and large cutoffs."""
+    p = uniform(20000, seed=3)
+    for r in (0.0, 1e-4, 1e-3, 0.05, 1.0):
+        got, _, _ = grid_knn(p, k, r)
+        assert torch.equal(got, oracle(p, k, r)), (k, r)
+
+
 def test_grid_knn_k_larger_than_n_and_tiny_sets():
     for n in (1, 2, 63, 64, 65, 130):
         p = uniform(n, seed=n)
