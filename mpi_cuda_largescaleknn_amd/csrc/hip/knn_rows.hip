@@ -120,7 +120,10 @@ constexpr int kPool = (kBins + 1) * 32;  // dwords per wave: histogram + trash r
 //  * no entry prefetch (0.129 vs 0.124 s), no early drain of a long row queue.
 constexpr int kTopBins = LSK_TOP_BINS;  // bins of the initial range above the estimate
 constexpr uint32_t kLogBins = kBins >= 64 ? 6 : kBins >= 32 ? 5 : 4;  // floor(log2(kBins))
-constexpr uint32_t kShift0 = 20;
+#ifndef LSK_ROWS_SHIFT0
+#define LSK_ROWS_SHIFT0 20
+#endif
+constexpr uint32_t kShift0 = LSK_ROWS_SHIFT0;
 constexpr uint32_t kMaxPasses = 96;
 constexpr uint32_t kGuardRounds = 1u << 22;
 // Step budget of a wave (all passes): max(kStepBudget, kStepsPerK * k) row-steps, ~16x
