@@ -408,7 +408,7 @@ def main():
     del pts_dev
     if rank == 0:
         if args.phases or args.stats:
-            print(json.dumps({"phases_s": info_last.timer.times, "counts": info_last.counts,
+            print(json.dumps({"phases_s": info_last.timer.times, "counts": info_last.plain_counts(),
                               "knn_stats": info_last.stats.counters}), file=sys.stderr)
         rec = {
             "metric": metric_name(n_total, args.k),
@@ -460,7 +460,7 @@ def instrumented_detail(comm, run_step, last_info) -> dict:
     step_s = time.perf_counter() - t0
     info = last_info()
     vec = [info.timer.times.get(p, 0.0) for p in PHASES] + [step_s] + \
-        [float(info.counts.get(c, 0)) for c in COUNTS]
+        [float(info.plain_counts().get(c, 0)) for c in COUNTS]
     allv = comm.allgather(torch.tensor(vec, dtype=torch.float64, device=comm.device)).cpu()
     np_ = len(PHASES)
     phases_max = {p: round(float(allv[:, i].max()) * 1e3, 3) for i, p in enumerate(PHASES)

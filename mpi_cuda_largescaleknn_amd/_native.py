@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 8  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 9  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -89,6 +89,7 @@ class KnnArgs(C.Structure):
         ("gate_on", C.c_int32),
         ("pad2", C.c_int32),
         ("ngroups_dev", vp),
+        ("wq", vp),
     ]
 
 

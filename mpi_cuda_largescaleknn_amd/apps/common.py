@@ -26,7 +26,7 @@ def write_stats(launch: Launch, args, info: PL.RunInfo, extra: dict, t_total: fl
     rec = {
         "rank": launch.rank,
         "phases_s": info.timer.times,
-        "counts": info.counts,
+        "counts": info.plain_counts(),
         "knn": info.stats.counters,
         "total_s": t_total,
         **extra,

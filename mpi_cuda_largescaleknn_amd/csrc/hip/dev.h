@@ -91,6 +91,16 @@ __device__ __forceinline__ uint32_t list_blocks(const Args &A, uint32_t nblk, ui
   return (uint32_t)min(need, (uint64_t)nblk);
 }
 
+// Next group of a persistent launch with a work queue (lsk_knn_args.wq, zeroed per
+// launch): lane 0 takes it with one global atomic, the wave shares it. Waves take groups
+// as they finish the previous one, so groups of very different cost (a short device-
+// counted list: the halo re-query) balance across the GPU instead of striding statically.
+__device__ __forceinline__ uint64_t wq_next(uint32_t *wq, uint32_t base) {
+  uint32_t w = 0;
+  if (lane_id() == 0) w = atomicAdd(wq, 1u);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)w) + base;
+}
+
 }  // namespace lsk
 
 // -------------------------------------------------------------------- host-side errors

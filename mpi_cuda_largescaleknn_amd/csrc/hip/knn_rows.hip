@@ -1085,11 +1085,15 @@ __global__ __launch_bounds__(kThreads, RCAP <= 32 ? LSK_ROWS_MINW : 4) void knn_
     uint64_t nwaves = A.groups ? (uint64_t)A.ngroups : (uint64_t)((A.nq + 63) / 64);
     if (A.groups && A.ngroups_dev) nwaves = min(nwaves, (uint64_t)*A.ngroups_dev);
     if (A.wave_end > 0) nwaves = min(nwaves, (uint64_t)A.wave_end);
-    for (uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid + (uint32_t)A.wave_base; w < nwaves;
-         w += (uint64_t)gridDim.x * kWavesPerBlock) {
+    // groups: strided, or from the work queue when the launch has one (A.wq)
+    const bool dyn = A.wq != nullptr;
+    uint64_t w = dyn ? lsk::wq_next(A.wq, (uint32_t)A.wave_base)
+                     : (uint64_t)blockIdx.x * kWavesPerBlock + wid + (uint32_t)A.wave_base;
+    while (w < nwaves) {
       [&](const uint64_t wave) {
 #include "knn_rows_wave.inc"
       }(w);
+      w = dyn ? lsk::wq_next(A.wq, (uint32_t)A.wave_base) : w + (uint64_t)gridDim.x * kWavesPerBlock;
     }
   }
 }

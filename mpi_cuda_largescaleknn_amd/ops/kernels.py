@@ -411,15 +411,23 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.fail_count = _ptr(count)
     a.fail_cap = cap
     full = 2 if short_list and groups is not None and ngroups_dev is not None else 0
+    # a short device-counted list runs persistent waves that take their groups from a work
+    # queue (one zeroed counter per launch): re-query groups differ widely in cost, and a
+    # static stride left the halo re-query at 9.1 vs 6.9 ms with the exact-size launch
+    # (1B / 8 ranks, scripts/rank_replay.py)
+    wqs = torch.zeros(2 * max(1, int(chunks)), dtype=torch.int32, device=qpts.device) if full else None
     nw = ngroups if groups is not None else (nq + BUCKET - 1) // BUCKET
     chunks = max(1, min(int(chunks), nw))
     # the pass as `chunks` consecutive launches over wave ranges (0 = to the end)
     spans = [(0, 0)] if chunks == 1 else [(nw * c // chunks, nw * (c + 1) // chunks) for c in range(chunks)]
+    def _wq(i: int, on: bool):
+        a.wq = _ptr(wqs[i:i + 1]) if on and wqs is not None else None
+
     if impl == "grid":
         slots, level, gbox, inf4 = grid[:4]
         gate = grid[4] if len(grid) > 4 else None
         gv = GridView(_ptr(slots), None, _ptr(gbox), _ptr(inf4), int(level), 0)
-        for a.wave_base, a.wave_end in spans:
+        for ci, (a.wave_base, a.wave_end) in enumerate(spans):
             if gate is not None:
                 # the device decides (lsk_hip_grid_decide): both kernels are queued, the one
                 # not chosen returns at its first instruction (no host read, graph-capturable)
@@ -428,19 +436,23 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
                 a.pad2 = full if expect_grid else 1
             else:
                 a.pad2 = full
+            _wq(2 * ci, a.pad2 == 2)
             check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
             if gate is not None:
                 a.gate_on = 0
                 a.pad2 = 1 if expect_grid else full
+                _wq(2 * ci + 1, a.pad2 == 2)
                 check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
             a.gate = None
             a.pad2 = 0
     else:
-        for a.wave_base, a.wave_end in spans:
+        for ci, (a.wave_base, a.wave_end) in enumerate(spans):
             a.pad2 = full
+            _wq(ci, a.pad2 == 2)
             check(lib.lsk_hip_knn_rows(C.byref(a), st), "knn_rows")
             a.pad2 = 0
     a.wave_base = a.wave_end = 0
+    a.wq = None
     # exact backstop over the failure list (device-side count: empty list = short no-op)
     check(lib.lsk_hip_knn_exact(C.byref(a), _ptr(flist), _ptr(count), cap, st), "knn_exact")
     return FailWord(count, cap)
