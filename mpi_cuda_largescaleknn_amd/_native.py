@@ -172,6 +172,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_knn_exact": ([C.POINTER(KnnArgs), vp, vp, i64, vp], i32),
         "lsk_hip_knn_rows": ([C.POINTER(KnnArgs), vp], i32),
         "lsk_hip_knn_grid": ([C.POINTER(KnnArgs), C.POINTER(GridView), vp], i32),
+        "lsk_hip_knn_grid2": ([C.POINTER(KnnArgs), C.POINTER(GridView), C.POINTER(GridView), vp], i32),
         "lsk_hip_grid_decide": ([vp, vp, i64, i32, C.c_float, i32, vp, vp], i32),
         "lsk_hip_boundary_groups": ([vp, i32, i64, vp, vp, vp, C.c_int, C.c_int, vp, vp], i32),
         "lsk_hip_grid_build": ([vp, vp, i64, vp, i32, vp, vp], i32),

@@ -340,6 +340,24 @@ struct GridCtx {
 #endif
 };
 
+// The grid fields of G from a view: the sorted points it indexes, its slots, the cube of
+// its keys (origin, quantisation) and the slack of its cell boundaries.
+__device__ __forceinline__ void load_grid(GridCtx &G, const lsk_grid_view &V, const float *pts) {
+  G.pts = pts;
+  G.inf4 = V.inf4;
+  G.slots = (const uint4 *)V.slots;
+  const lsk::cfloat_p bx = lsk::as_const(V.box);
+  G.ox = bx[0];
+  G.oy = bx[1];
+  G.oz = bx[2];
+  G.scale = bx[6];
+  const float ext = bx[7];
+  G.step = ext * (1.f / 1024.f);
+  const float mag = fmaxf(fmaxf(fabsf(G.ox), fabsf(G.oy)), fmaxf(fabsf(G.oz), 0.f)) + ext;
+  G.eps = mag * 0x1p-19f;
+  G.lc = (uint32_t)V.level;
+}
+
 // The histogram add's operands after a change of the lane's range or state. A lane that
 // is not histogramming adds 0 (to its row 0).
 __device__ __forceinline__ void hist_regs(Lane &s, const GridCtx &G) {
@@ -1107,14 +1125,37 @@ __device__ bool grid_pass_impl(Lane &s, GridCtx &G, uint32_t n) {
   return true;
 }
 
+// One pass over every candidate source: the index's own grid, then (NG = 2: the halo
+// re-query of a distributed run) the grid of the received halo points, whose
+// cells are walked the same way from the same wave box and (shrinking) radius; the
+// histogram / collect pool spans both. G ends on the first grid.
+template <int MODE, int NG>
+__device__ __forceinline__ bool grid_pass_n(Lane &s, GridCtx &G, const lsk_knn_args &A, const lsk_grid_view &V,
+                                            const lsk_grid_view &V1) {
+  bool ok = grid_pass<MODE>(s, G, (uint32_t)A.tree[0].n);
+  if (NG > 1) {
+    load_grid(G, V1, A.tree[1].pts);
+    ok = ok && grid_pass<MODE>(s, G, (uint32_t)A.tree[1].n);
+    load_grid(G, V, A.tree[0].pts);
+  }
+  return ok;
+}
+
 // STRIDE = false: one wave per group (the normal launch). STRIDE = true: a small persistent
 // grid strides over the groups — the form launched when the device gate is expected to
 // pick knn_rows: every wave returns at once when it does, instead of millions of blocks
 // each being dispatched only to return (1B points: ~16 ms per launch); and, at full
 // occupancy, over a group list whose device-side length is far below its bound (a rank's
 // boundary groups: ~5 % of its groups).
-template <bool STRIDE>
-__global__ __launch_bounds__(kThreads, LSK_GRID_MINW) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V) {
+#ifndef LSK_GRID2_MINW
+#define LSK_GRID2_MINW 4  // waves/SIMD of the two-source form (at 6: 393 SGPR / 146 VGPR spills)
+#endif
+#ifndef LSK_GRID_STRIDE_MINW
+#define LSK_GRID_STRIDE_MINW LSK_GRID_MINW
+#endif
+template <bool STRIDE, int NG>
+__global__ __launch_bounds__(kThreads, NG > 1 ? LSK_GRID2_MINW : (STRIDE ? LSK_GRID_STRIDE_MINW : LSK_GRID_MINW)) void knn_grid_kernel(const lsk_knn_args A, const lsk_grid_view V,
+                                                                          const lsk_grid_view V1) {
   __shared__ uint32_t lds[kWPB][kPool + 8 * kCullGroups];
   const int wid = threadIdx.x >> 6;
   const int lane = lsk::lane_id();
@@ -1308,16 +1349,19 @@ extern "C" int lsk_hip_grid_sq(const uint32_t *slots, int64_t nslot, unsigned lo
   return 0;
 }
 
-extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *stream) {
+static int knn_grid_launch(const lsk_knn_args *args, const lsk_grid_view *grid, const lsk_grid_view *grid1,
+                           void *stream) {
   const lsk_knn_args &A = *args;
   if (A.k < 1 || A.k > 65535) {
     lsk::set_last_error("knn_grid: k must be in [1, 65535]");
     return 1;
   }
-  if (A.nq >= ((int64_t)1 << 32) || A.ntrees != 1 || A.init_d2 || A.tree[0].n >= ((int64_t)1 << 32) ||
-      !grid || grid->level < 0 || grid->level > 8) {
-    lsk::set_last_error("knn_grid: one tree (< 2^32 points, the queries' own), no init_d2, "
-                        "grid level in [0, 8]");
+  const int ng = grid1 ? 2 : 1;
+  if (A.nq >= ((int64_t)1 << 32) || A.ntrees != ng || (ng == 1 && A.init_d2) || A.tree[0].n >= ((int64_t)1 << 32) ||
+      (ng == 2 && A.tree[1].n >= ((int64_t)1 << 32)) || !grid || grid->level < 0 || grid->level > 8 ||
+      (grid1 && (grid1->level < 0 || grid1->level > 8))) {
+    lsk::set_last_error("knn_grid: one tree and grid (< 2^32 points, the queries' own; no init_d2), or two "
+                        "(knn_grid2: + the halo's), grid levels in [0, 8]");
     return 1;
   }
   const int64_t ngroups = A.groups ? A.ngroups : (A.nq + 63) / 64;
@@ -1325,12 +1369,34 @@ extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *g
   const int64_t wend = A.wave_end > 0 && A.wave_end < ngroups ? A.wave_end : ngroups;
   if (A.wave_base < 0 || wend - A.wave_base <= 0) return 0;
   const unsigned nblk = lsk_blocks(wend - A.wave_base, kWPB);
-  if (A.pad2 >= 1) {  // persistent strided form (see knn_grid_kernel); 2: a short list
-    const unsigned cap = A.pad2 == 2 ? kStrideBlocksFull : kStrideBlocks;
-    knn_grid_kernel<true><<<nblk < cap ? nblk : cap, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
+  const unsigned cap = A.pad2 == 2 ? kStrideBlocksFull : kStrideBlocks;
+  const unsigned sblk = nblk < cap ? nblk : cap;
+  hipStream_t st = (hipStream_t)stream;
+  if (ng == 2) {  // (the halo re-query: a device-counted list, persistent or full form)
+    if (A.pad2 >= 1)
+      knn_grid_kernel<true, 2><<<sblk, kThreads, 0, st>>>(A, *grid, *grid1);
+    else
+      knn_grid_kernel<false, 2><<<nblk, kThreads, 0, st>>>(A, *grid, *grid1);
+  } else if (A.pad2 >= 1) {  // persistent strided form (see knn_grid_kernel); 2: a short list
+    knn_grid_kernel<true, 1><<<sblk, kThreads, 0, st>>>(A, *grid, *grid);
+  } else {
+    knn_grid_kernel<false, 1><<<nblk, kThreads, 0, st>>>(A, *grid, *grid);
   }
-  else
-    knn_grid_kernel<false><<<nblk, kThreads, 0, (hipStream_t)stream>>>(A, *grid);
   LSK_CHECK_LAUNCH("knn_grid");
   return 0;
+}
+
+extern "C" int lsk_hip_knn_grid(const lsk_knn_args *args, const lsk_grid_view *grid, void *stream) {
+  return knn_grid_launch(args, grid, nullptr, stream);
+}
+
+// The halo re-query on the grid: args->tree[1] / grid1 are the received halo
+// points' index and grid; args->init_d2 (optional) the local k-th as an upper bound.
+extern "C" int lsk_hip_knn_grid2(const lsk_knn_args *args, const lsk_grid_view *grid, const lsk_grid_view *grid1,
+                                 void *stream) {
+  if (!grid1) {
+    lsk::set_last_error("knn_grid2: the halo grid view is required");
+    return 1;
+  }
+  return knn_grid_launch(args, grid, grid1, stream);
 }

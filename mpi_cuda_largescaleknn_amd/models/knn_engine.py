@@ -144,13 +144,14 @@ class KnnStats:
 
 def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
                 keys: tuple | None = None, grid: bool = False, density_n: int | None = None,
-                grid_level: int | None = None) -> LocalIndex:
+                grid_level: int | None = None, grid_gated: bool = True) -> LocalIndex:
     """Sort points along the space-filling curve of `box` (default: their own bounds) and
     build the bucket tree. `keys` = (keys, iota) computed already (SetStream's PRE_KEYS:
     the next set's box and curve keys on the side stream beside the current k-NN). `grid`: also index the sorted points by the cell grid of
     the fast local k-NN pass (build_grid, GPU). `density_n`: the number of points that
     fill `box` (a rank's share of a global box: the global count; default: n).
-    `grid_level` (tests): force the grid's grandchild level.
+    `grid_level`: force the grid's grandchild level (tests; a halo index takes the local
+    grid's); `grid_gated=False`: no census / device gate for the grid (build_grid).
     No host read on the way unless an over-full key cell needs the eager refinement
     (refine_heavy_cells; under host_sync_free() not even that)."""
     points = points.contiguous()
@@ -173,7 +174,7 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     index = LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
     if grid:
         index.grid = build_grid(index, skeys, density_n, grid_level,
-                                counts=census[0] if census is not None else None)
+                                counts=census[0] if census is not None else None, gated=grid_gated)
     return index
 
 
@@ -224,7 +225,8 @@ def grid_applies(distinct: list[int], n: int, g: int) -> bool:
 
 
 def build_grid(index: LocalIndex, skeys: torch.Tensor, density_n: int | None = None,
-               level: int | None = None, counts: torch.Tensor | None = None) -> GridIndex | None:
+               level: int | None = None, counts: torch.Tensor | None = None,
+               gated: bool = True) -> GridIndex | None:
     """Cell grid over index's sorted points (knn_grid.hip), or None (CPU, GRID=off).
 
     The level comes from the point counts (grid_level_for); whether the grid applies is
@@ -232,14 +234,15 @@ def build_grid(index: LocalIndex, skeys: torch.Tensor, density_n: int | None = N
     crowding sum — clustered or multi-scale data keeps the bucket-tree walk of knn_rows,
     which adapts to density): the k-NN launch queues both kernels and the device runs the
     chosen one. No host read, so the build is graph-capturable and a stream of sets never
-    waits for the previous set's k-NN here."""
+    waits for the previous set's k-NN here. `gated=False` (a halo index: whether its grid
+    serves is the local index's gate): no census, no gate."""
     n = index.n
     if GRID == "off" or n == 0 or not K.is_gpu(index.pts):
         return None
     g = level if level is not None else grid_level_for(density_n if density_n is not None else n, n)
     slots = K.grid_build(index.pts, skeys, n, index.box, g - 2)
     gate = None
-    if GRID == "auto":
+    if GRID == "auto" and gated:
         if counts is None:
             counts = K.key_levels_dev(skeys[:n])
         sq = K.grid_sq_dev(slots)
@@ -508,8 +511,12 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     kw = dict(groups=groups, ngroups=ngroups, seed=SEED_BUCKETS, init_d2=init_d2,
               out_perm=index.perm if final_out is not None else None, out_final=final_out)
     impl = KNN_IMPL
-    use_grid = (impl == "rows" and index.grid is not None and len(trees) == 1
-                and init_d2 is None and cfg.k <= K.ROWS_MAX_K)
+    # two grids: the halo re-query of a distributed run (the halo index has a grid of its
+    # own, pipelines._halo_requery); the local index's gate still picks grid or rows
+    two_grid = (impl == "rows" and index.grid is not None and len(trees) == 2 and extra.grid is not None
+                and cfg.k <= K.ROWS_MAX_K)
+    use_grid = two_grid or (impl == "rows" and index.grid is not None and len(trees) == 1
+                            and init_d2 is None and cfg.k <= K.ROWS_MAX_K)
     if len(trees) == 1 and init_d2 is None:  # (a local pass, not a halo re-query)
         if use_grid and index.grid.gate is not None:
             GATES_SEEN.append(index.grid.gate)  # grid or rows: resolved by kernels_used()
@@ -520,7 +527,8 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     fw = K.knn_gpu(index.pts, n, trees, cfg.k, cfg.cut2, hint2, out, stats=raw, qstatus=qstatus,
                    impl="grid" if use_grid else impl, debug_fail_mod=DEBUG_FAIL_MOD,
                    grid=index.grid.view() if use_grid else None, ngroups_dev=ngroups_dev,
-                   expect_grid=GRID_EXPECT[0], short_list=short_list, chunks=chunks, **kw)
+                   expect_grid=GRID_EXPECT[0], short_list=short_list, chunks=chunks,
+                   grid2=extra.grid.view()[:4] if two_grid else None, **kw)
     gate = index.grid.gate if use_grid else None
     def check() -> bool:
         # one 4-byte read: failures beyond the list capacity (pathological input) rerun

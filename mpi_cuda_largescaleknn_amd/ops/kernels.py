@@ -330,7 +330,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
             debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None,
-            expect_grid: bool = True, short_list: bool = False, chunks: int = 1) -> FailWord:
+            expect_grid: bool = True, short_list: bool = False, chunks: int = 1, grid2=None) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -361,6 +361,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     cell-grid candidate source of knn_grid.hip for one tree whose points are the queries
     (same failure list and backstop as "rows"); with a device gate (int32 [1]) the grid
     kernel runs iff gate == 1 and knn_rows iff gate == 0.
+    grid2 (impl "grid", two trees: the halo re-query): the second tree's grid (slots, level,
+    box, inf4) — knn_grid2 walks both grids; init_d2 is allowed then.
     Returns the launch's FailWord.
     """
     if (out_perm is None) != (out_final is None):
@@ -370,8 +372,9 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
         raise ValueError("knn_gpu: out_perm must be int32 [>= nq], out_final float32")
     if impl not in ("rows", "exact", "grid"):
         raise ValueError(f"knn_gpu: impl must be rows, exact or grid, not {impl!r}")
-    if impl == "grid" and (grid is None or len(trees) != 1 or init_d2 is not None):
-        raise ValueError("knn_gpu: impl grid needs a grid, one tree and no init_d2")
+    if impl == "grid" and (grid is None or len(trees) != (2 if grid2 is not None else 1)
+                           or (grid2 is None and init_d2 is not None)):
+        raise ValueError("knn_gpu: impl grid needs a grid and one tree (no init_d2), or two trees and grid2")
     a = KnnArgs()
     a.qpts = _ptr(qpts)
     a.nq = nq
@@ -427,6 +430,7 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
         slots, level, gbox, inf4 = grid[:4]
         gate = grid[4] if len(grid) > 4 else None
         gv = GridView(_ptr(slots), None, _ptr(gbox), _ptr(inf4), int(level), 0)
+        gv2 = GridView(_ptr(grid2[0]), None, _ptr(grid2[2]), _ptr(grid2[3]), int(grid2[1]), 0) if grid2 is not None else None
         for ci, (a.wave_base, a.wave_end) in enumerate(spans):
             if gate is not None:
                 # the device decides (lsk_hip_grid_decide): both kernels are queued, the one
@@ -437,7 +441,10 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             else:
                 a.pad2 = full
             _wq(2 * ci, a.pad2 == 2)
-            check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
+            if gv2 is not None:
+                check(lib.lsk_hip_knn_grid2(C.byref(a), C.byref(gv), C.byref(gv2), st), "knn_grid2")
+            else:
+                check(lib.lsk_hip_knn_grid(C.byref(a), C.byref(gv), st), "knn_grid")
             if gate is not None:
                 a.gate_on = 0
                 a.pad2 = 1 if expect_grid else full

@@ -448,17 +448,42 @@ def _halo_send(index: E.LocalIndex, radii_nodes: torch.Tensor, comm: Comm, cfg: 
     return recv
 
 
+# The halo re-query on knn_grid2 (two grids: local + halo, see halo_index) instead of the
+# bucket-tree kernel with two trees. 1B / 8 ranks, per-rank replay (profiles/r6_rank): the
+# re-query launch 6.2 ms (rows) -> 4.85 ms with the halo grid one level coarser than the
+# local one (its shell of points is thin: at the local level 2.4x the cells per wave, 5.8
+# ms); the grid build adds ~0.4 ms; per-rank total 122.4 -> 120.5 ms. 0: knn_rows.
+HALO_GRID = os.environ.get("LSKNN_HALO_GRID", "1") != "0"
+HALO_GRID_DLEVEL = int(os.environ.get("LSKNN_HALO_GRID_DLEVEL", "-1"))  # halo grid level - local level
+# the re-query's first range ends at the local k-th (0: the density estimate instead; A/B at
+# 1B / 8: rows 6.2 vs 7.1 ms, grid 6.2 vs 6.5)
+REQUERY_BOUND = os.environ.get("LSKNN_REQUERY_BOUND", "1") != "0"
+
+
+def halo_index(index: E.LocalIndex, recv: torch.Tensor) -> E.LocalIndex:
+    """Index of the received halo points. With a local grid the halo points get a grid of
+    their own at the local grid's level (no gate: the local index's gate decides for both),
+    so the re-query runs on the grid kernel over both sources when the local pass did
+    (knn_grid2); the bucket-tree kernel with two trees otherwise."""
+    g = HALO_GRID and index.grid is not None
+    lvl = max(2, index.grid.level + 2 + HALO_GRID_DLEVEL) if g else None
+    return E.build_index(recv, grid=g, grid_level=lvl, grid_gated=False)
+
+
 def _halo_requery(index: E.LocalIndex, d2: torch.Tensor, recv: torch.Tensor, cfg: E.KnnConfig,
-                  hint2: float | torch.Tensor, info: RunInfo, final_out: torch.Tensor | None) -> torch.Tensor:
-    """Halo tree from the received points; re-query (against local + halo) every query
-    group a halo point can reach within its local k-th radius (index.nodes must carry the
-    final radii: tree_set_radii). Updates d2 / final_out in place."""
+                  hint2: float | torch.Tensor, info: RunInfo, final_out: torch.Tensor | None,
+                  hidx: E.LocalIndex | None = None) -> torch.Tensor:
+    """Halo index from the received points (`hidx`: built already); re-query (against
+    local + halo) every query group a halo point can reach within its local k-th radius
+    (index.nodes must carry the final radii: tree_set_radii). Updates d2 / final_out in
+    place."""
     n = index.n
     dev = index.device
     nh = recv.shape[0]
     if nh == 0 or n == 0:
         return d2
-    hidx = E.build_index(recv)
+    if hidx is None:
+        hidx = halo_index(index, recv)
     if K.is_gpu(index.pts):
         from .. import _native
         lib = _native.hip()
@@ -479,7 +504,8 @@ def _halo_requery(index: E.LocalIndex, d2: torch.Tensor, recv: torch.Tensor, cfg
         # the local k-th distance bounds the true one from above: the re-query starts with
         # a tight first range
         E.query(index, cfg, hint2, extra=hidx, groups=glist, ngroups=ng, ngroups_dev=cnt, short_list=True,
-                out=d2, stats=info.stats if cfg.collect_stats else None, init_d2=d2, final_out=final_out)
+                out=d2, stats=info.stats if cfg.collect_stats else None, init_d2=d2 if REQUERY_BOUND else None,
+                final_out=final_out)
     else:
         info.timer.mark("halo_tree")
         E.query(index, cfg, hint2, extra=hidx, out=d2, final_out=final_out)

@@ -12,7 +12,7 @@ and timed with events, as it would run on its own MI355X:
            published trees
   local    the local k-NN pass (boundary groups, then interior groups)
   halo     halo filter of the rank's points against the other ranks' published radii
-           (what it sends) + the halo tree of what it received
+           (what it sends) + the index (tree + grid) of what it received
   requery  flagging + re-query of the groups a received point can reach
   return   the result scatter back to input order (the all-to-all-v itself is xGMI time)
 
@@ -20,6 +20,7 @@ and the halo sizes. Prints one line per rank and a JSON summary (max over ranks)
 collectives' xGMI time is not included (no peers here); see BASELINE.md for the model.
 """
 import json
+import os
 import sys
 import time
 
@@ -155,13 +156,48 @@ for r in range(P):
     pub2, dep2, off2 = st["pubs"][1]
     mask, t_mask = timed(lambda: K.halo_mask(index.pts[:nr], pub2.reshape(-1), off2, dep2, r))
     recv = st["recv"]
-    hidx, t_htree = timed(lambda: E.build_index(recv) if recv.shape[0] else None)
+    # (the halo index as the pipeline builds it: with a grid at the local level; timed
+    # here, not again inside the re-query — round 5's replay counted it twice)
+    hidx, t_htree = timed(lambda: PL.halo_index(index, recv) if recv.shape[0] else None)
     K.tree_set_radii(index.nodes, nr, d2)
 
     def requery():
         info = PL.RunInfo(PL.PhaseTimer(False, DEV))
-        PL._halo_requery(index, d2, recv, cfg, hint2, info, fin)
+        PL._halo_requery(index, d2, recv, cfg, hint2, info, fin, hidx=hidx)
         return info.counts.get("requery_groups", 0)
+
+    if os.environ.get("REPLAY_REQUERY_STATS") and r == 0:
+        # (untimed) kernel counters of the re-query: evaluations, passes, backstop
+        d2s = d2.clone()
+        info = PL.RunInfo(PL.PhaseTimer(False, DEV))
+        PL._halo_requery(index, d2s, recv, E.KnnConfig(k=cfg.k, collect_stats=True), hint2, info, fin.clone(),
+                         hidx=hidx)
+        c = info.stats.counters
+        w = max(c.get("waves", 1), 1)
+        # flagging + compaction vs the re-query launch (device-synchronised marks, 2nd run)
+        tinfo = PL.RunInfo(PL.PhaseTimer(True, DEV))
+        tinfo.timer.start()
+        PL._halo_requery(index, d2.clone(), recv, cfg, hint2, tinfo, fin.clone(), hidx=hidx)
+        print("requery phases ms:", {kk: round(v * 1e3, 2) for kk, v in tinfo.timer.times.items()}, flush=True)
+        # the same flagged groups through the local pass alone (one tree, no bound), and
+        # as many interior groups: is it the groups or the second source?
+        hflags = torch.zeros(ng, dtype=torch.int32, device=DEV)
+        K.check(K._native.hip().lsk_hip_flag_groups_inverse(hidx.pts.data_ptr(), hidx.n, index.nodes.data_ptr(),
+                                                            index.depth, ng, hflags.data_ptr(),
+                                                            K._stream(index.pts)), "flag_groups")
+        hl, hc = K.compact_flags(hflags)
+        il = ilist[:int(hc.item())].contiguous()
+        ic = torch.tensor([il.numel()], dtype=torch.int32, device=DEV)
+        dd = d2.clone()
+        for nm, gl, gc in (("flagged", hl, hc), ("interior", il, ic)):
+            _, tq = timed(lambda: E.query(index, cfg, hint2, out=dd, groups=gl, ngroups=ng, ngroups_dev=gc,
+                                          short_list=True))
+            print(f"local pass over {int(gc.item())} {nm} groups: {tq:.2f} ms", flush=True)
+        print("requery stats:", {kk: c.get(kk, 0) for kk in ("waves", "fallback_queries", "failed_lanes",
+                                                             "overflow_lanes", "underflow_lanes")},
+              f"evals/w {c.get('evals', 0) / w:.0f} passes/w {c.get('hist_passes', 0) / w:.2f} "
+              f"cells/w {c.get('leaves', 0) / w:.1f}", flush=True)
+        del d2s
 
     nreq, t_req = timed(requery)
     res = torch.empty(nr, dtype=torch.float32, device=DEV)

@@ -282,3 +282,65 @@ def test_chunked_pass_equals_one_launch(gen, monkeypatch):
     rows = (lst[:cnt.item()].long()[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
     rows = rows[rows < idx.n]
     assert torch.equal(outs[1].cpu()[rows], one.cpu()[rows])
+
+
+def _two_source(p, h, k, r=math.inf, groups=None, grid_halo=True, init=True):
+    """Local index over p, halo index over h (with a grid at the local level unless
+    grid_halo=False), a local pass, then the re-query of `groups` (all: None) against both
+    sources with the local k-th as the upper bound — the distributed halo re-query."""
+    old = E.GRID
+    E.GRID = "on"
+    try:
+        cfg = E.KnnConfig(k=k, max_radius=r)
+        idx = E.build_index(p.to(DEV), grid=True)
+        hidx = E.build_index(h.to(DEV), grid=grid_halo, grid_level=idx.grid.level + 2 if grid_halo else None,
+                             grid_gated=False)
+        hint = E.radius_hint(idx.box, idx.n, k)
+        d2 = E.query(idx, cfg, hint)
+        ng = (idx.n + 63) // 64
+        if groups is None:
+            groups = torch.arange(ng, dtype=torch.int32, device=DEV)
+        cnt = torch.tensor([groups.numel()], dtype=torch.int32, device=DEV)
+        st = E.KnnStats()
+        out = d2.clone()
+        E.query(idx, cfg, hint, extra=hidx, groups=groups, ngroups=ng, ngroups_dev=cnt, short_list=True,
+                out=out, init_d2=d2.clone() if init else None, stats=st)
+        return out, d2, idx, st
+    finally:
+        E.GRID = old
+
+
+@pytest.mark.parametrize("k", [1, 16, 100])
+def test_grid_two_sources_match_oracle(k):
+    """knn_grid2 (the halo re-query on the grid: local grid + the halo's own grid, the
+    local k-th as the first range's top): bitwise equal to the CPU oracle over the union,
+    with a cutoff, and equal to the bucket-tree kernel's two-tree re-query."""
+    p = uniform(60_000, seed=11)
+    h = uniform(8_000, seed=12) * 0.3 + torch.tensor([1.0, 0.2, 0.4])  # a slab beside p's cube
+    allp = torch.cat([p, h])
+    for r in (math.inf, 0.03):
+        out, _, idx, st = _two_source(p, h, k, r)
+        ref = K.kth_cpu(allp, idx.pts[:idx.n].cpu(), k, E.cut2_of(r))
+        assert torch.equal(out.cpu().view(torch.int32), ref.view(torch.int32)), (k, r)
+        assert st.counters.get("fallback_queries", 0) == 0
+        rows, _, _, _ = _two_source(p, h, k, r, grid_halo=False)
+        assert torch.equal(out.cpu().view(torch.int32), rows.cpu().view(torch.int32)), (k, r)
+
+
+def test_grid_two_sources_listed_groups_and_no_bound():
+    """Only listed groups change; without the upper bound (init_d2) the two-source pass
+    starts from the density estimate and gives the same bits."""
+    k = 24
+    p = uniform(40_000, seed=21)
+    h = uniform(5_000, seed=22) * torch.tensor([0.2, 1.0, 1.0]) + torch.tensor([-0.2, 0.0, 0.0])
+    groups = torch.arange(0, (40_000 + 63) // 64, 3, dtype=torch.int32, device=DEV)
+    out, d2, idx, _ = _two_source(p, h, k, groups=groups)
+    nob, _, _, _ = _two_source(p, h, k, groups=groups, init=False)
+    assert torch.equal(out.view(torch.int32), nob.view(torch.int32))
+    rows = (groups.to(torch.int64)[:, None] * 64 + torch.arange(64, device=DEV)[None, :]).reshape(-1)
+    rows = rows[rows < idx.n].cpu()
+    ref = K.kth_cpu(torch.cat([p, h]), idx.pts[:idx.n].cpu()[rows], k, math.inf)
+    assert torch.equal(out.cpu()[rows].view(torch.int32), ref.view(torch.int32))
+    keep = torch.ones(idx.n, dtype=torch.bool)
+    keep[rows] = False
+    assert torch.equal(out.cpu()[keep], d2.cpu()[keep])  # unlisted groups untouched
