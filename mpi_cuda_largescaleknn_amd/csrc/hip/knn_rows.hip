@@ -995,6 +995,9 @@ __device__ __forceinline__ float bcast64(float v, uint32_t j) {
 // mixed-scale data: 99.99 % of groups >= 3.5e-3, worst 7e-7), points on a plane give
 // det ~ 0 (<= 2e-11 tilted, exactly 0 axis-aligned) and points on a line also give the sum
 // of the 2x2 principal minors ~ 0 (<= 7e-9; planes >= 1e-4). 3, 2 or 1.
+#ifndef LSK_DIM2_MIN
+#define LSK_DIM2_MIN 1e-5
+#endif
 __device__ __forceinline__ uint32_t group_dimension(const Lane &s, bool valid, uint32_t nvalid) {
   const float inv = 1.f / (float)(nvalid > 0 ? nvalid : 1u);
   const float mx = lsk::wave_sum_f(valid ? s.qx : 0.f) * inv, my = lsk::wave_sum_f(valid ? s.qy : 0.f) * inv,
@@ -1009,7 +1012,12 @@ __device__ __forceinline__ uint32_t group_dimension(const Lane &s, bool valid, u
   const float m_xy = cxx * cyy - cxy * cxy, m_xz = cxx * czz - cxz * cxz, m_yz = cyy * czz - cyz * cyz;
   const float det = cxx * m_yz - cxy * (cxy * czz - cyz * cxz) + cxz * (cxy * cyz - cyy * cxz);
   if (det >= 1e-6f) return 3u;
-  return m_xy + m_xz + m_yz >= 1e-5f ? 2u : 1u;
+  // (LSK_DIM2_MIN, round 6: 1e-2 / 1e-3 classify a line of float-quantised points — its
+  // coordinates rounded by up to half an ulp across it, ~1e-3 here — as 1-D: 2e7 line,
+  // k = 100, 702 -> 785 / 746 Mpts/s, but clustered 594 -> 405 / 410: groups that straddle
+  // a curve discontinuity between two clumps look like lines too and get the 1-D scale;
+  // kept at 1e-5, profiles/r6_nonuniform/)
+  return m_xy + m_xz + m_yz >= (float)LSK_DIM2_MIN ? 2u : 1u;
 }
 
 __device__ __forceinline__ float own_group_estimate(const Lane &s, uint32_t nvalid, uint32_t k,
