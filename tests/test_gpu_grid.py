@@ -274,11 +274,15 @@ def test_chunked_pass_equals_one_launch(gen, monkeypatch):
     full = torch.full((ng,), -1, dtype=torch.int32)
     full[:lst.numel()] = lst
     outs = []
-    for c in (1, 4):
+    # (short_list: the persistent form, whose waves take groups from one work-queue
+    # counter per launch — four chunks, four counters)
+    for c, sl in ((1, False), (4, False), (1, True), (4, True)):
         d2 = torch.zeros(idx.n, device=DEV)
-        E.query(idx, cfg, hint2, out=d2, groups=full.to(DEV), ngroups=ng, ngroups_dev=cnt.to(DEV), chunks=c)
+        E.query(idx, cfg, hint2, out=d2, groups=full.to(DEV), ngroups=ng, ngroups_dev=cnt.to(DEV), chunks=c,
+                short_list=sl)
         outs.append(d2)
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     rows = (lst[:cnt.item()].long()[:, None] * 64 + torch.arange(64)[None, :]).reshape(-1)
     rows = rows[rows < idx.n]
     assert torch.equal(outs[1].cpu()[rows], one.cpu()[rows])
