@@ -163,6 +163,7 @@ def _declare_hip(lib: C.CDLL) -> None:
         "lsk_hip_sort_ws_bytes": ([i64], C.c_size_t),
         "lsk_hip_sort_pairs": ([vp, vp, vp, vp, i64, i32, vp, C.POINTER(C.c_int), vp], i32),
         "lsk_hip_sort_keys_iota": ([vp, vp, vp, vp, i64, i32, vp, C.POINTER(C.c_int), vp], i32),
+        "lsk_hip_sort_keys_iota_gather": ([vp, vp, vp, vp, i64, i32, vp, C.POINTER(C.c_int), vp, vp, vp], i32),
         "lsk_hip_key_census": ([vp, i64, vp, i64, vp, vp], i32),
         "lsk_hip_tree_depth": ([i64], i32),
         "lsk_hip_tree_nodes": ([i64], i64),

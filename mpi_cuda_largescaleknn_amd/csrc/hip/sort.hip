@@ -139,10 +139,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(uint32_t *__restrict
 // 6.6 ms per pass for 1B pairs (2.4 TB/s). Loading tile t+1 while tile t is written out
 // (208 VGPRs) and a 4-waves/SIMD occupancy hint (66 VGPRs spilled) measured the same
 // (profiles/r5_sort/).
+// GATHER (the last pass of lsk_hip_sort_keys_iota_gather): the values are the points'
+// input rows; every element's point is read from pin and written at its sorted position
+// in pout as the pair is scattered (the separate gather3 pass and its read of the
+// permutation fused into the sort).
+template <bool GATHER>
 __global__ __launch_bounds__(kThreads) void downsweep_kernel(
     const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int64_t n, int shift,
-    const uint32_t *__restrict__ offsets) {
+    const uint32_t *__restrict__ offsets, const float *__restrict__ pin, float *__restrict__ pout) {
   __shared__ uint32_t wave_cnt[kWaves][kRadix];
   __shared__ uint32_t run_base[kRadix];
   __shared__ uint32_t tile_start[kRadix];
@@ -212,12 +217,49 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(
       }
     }
     __syncthreads();
-    for (int i = t; i < tn; i += kThreads) {
-      const uint32_t k = stage_k[i];
-      const uint32_t d = (k >> shift) & 255u;
-      const uint32_t g = run_base[d] + (uint32_t)i - tile_start[d];
-      kout[g] = k;
-      vout[g] = stage_v[i];
+    if (GATHER) {
+      // four elements per thread in flight: their random 12-byte point reads overlap
+      constexpr int kU = 4;
+      for (int i0 = t; i0 < tn; i0 += kU * kThreads) {
+        uint32_t gg[kU], vv[kU];
+        float x[kU], y[kU], z[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const int i = i0 + u * kThreads;
+          const uint32_t k = i < tn ? stage_k[i] : 0u;
+          const uint32_t d = (k >> shift) & 255u;
+          gg[u] = run_base[d] + (uint32_t)i - tile_start[d];
+          vv[u] = i < tn ? stage_v[i] : 0u;
+          if (i < tn) {
+            kout[gg[u]] = k;
+            vout[gg[u]] = vv[u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const float *p = pin + 3ull * vv[u];  // (row 0 for the padding slots: in bounds)
+          x[u] = p[0];
+          y[u] = p[1];
+          z[u] = p[2];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          if (i0 + u * kThreads < tn) {
+            float *q = pout + 3ull * gg[u];
+            q[0] = x[u];
+            q[1] = y[u];
+            q[2] = z[u];
+          }
+        }
+      }
+    } else {
+      for (int i = t; i < tn; i += kThreads) {
+        const uint32_t k = stage_k[i];
+        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t g = run_base[d] + (uint32_t)i - tile_start[d];
+        kout[g] = k;
+        vout[g] = stage_v[i];
+      }
     }
     __syncthreads();
     run_base[t] += tile_total[t];
@@ -234,7 +276,8 @@ extern "C" size_t lsk_hip_sort_ws_bytes(int64_t n) {
 }
 
 static int sort_impl(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, int64_t n,
-                     int key_bits, void *ws, int *result_in_alt, bool iota, void *stream) {
+                     int key_bits, void *ws, int *result_in_alt, bool iota, void *stream,
+                     const float *pin = nullptr, float *pout = nullptr) {
   hipStream_t s = (hipStream_t)stream;
   *result_in_alt = 0;
   if (n <= 1 || key_bits <= 0) return 0;
@@ -251,7 +294,11 @@ static int sort_impl(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_
     LSK_CHECK_LAUNCH("sort_upsweep");
     scan_kernel<<<1, 1024, 0, s>>>(counts, (int64_t)kRadix * nb);
     LSK_CHECK_LAUNCH("sort_scan");
-    downsweep_kernel<<<nb, kThreads, 0, s>>>(ki, (iota && passes == 0) ? nullptr : vi, ko, vo, n, shift, counts);
+    const uint32_t *vsrc = (iota && passes == 0) ? nullptr : vi;
+    if (pin && shift + 8 >= key_bits)  // the last pass: scatter the points too
+      downsweep_kernel<true><<<nb, kThreads, 0, s>>>(ki, vsrc, ko, vo, n, shift, counts, pin, pout);
+    else
+      downsweep_kernel<false><<<nb, kThreads, 0, s>>>(ki, vsrc, ko, vo, n, shift, counts, nullptr, nullptr);
     LSK_CHECK_LAUNCH("sort_downsweep");
     std::swap(ki, ko);
     std::swap(vi, vo);
@@ -276,4 +323,16 @@ extern "C" int lsk_hip_sort_keys_iota(uint32_t *keys, uint32_t *vals, uint32_t *
     return 0;
   }
   return sort_impl(keys, vals, keys_alt, vals_alt, n, key_bits, ws, result_in_alt, true, stream);
+}
+
+// As lsk_hip_sort_keys_iota, and pout[j] = pin[perm[j]] (float3 rows) for the sorted
+// order, written by the last pass (no separate gather). n >= 2 (one point: gather3).
+extern "C" int lsk_hip_sort_keys_iota_gather(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt,
+                                             int64_t n, int key_bits, void *ws, int *result_in_alt, const float *pin,
+                                             float *pout, void *stream) {
+  if (n < 2 || key_bits <= 0 || !pin || !pout) {
+    lsk::set_last_error("sort_keys_iota_gather: n >= 2, key_bits > 0 and both point arrays required");
+    return 1;
+  }
+  return sort_impl(keys, vals, keys_alt, vals_alt, n, key_bits, ws, result_in_alt, true, stream, pin, pout);
 }

@@ -142,6 +142,12 @@ class KnnStats:
         self.counters["fallback_queries"] = self.counters.get("fallback_queries", 0) + int(n)
 
 
+# The point gather fused into the key sort's last pass (kernels.sort_keys_iota_gather)
+# instead of a gather3 pass over the permutation: 1B build 74.9 vs 71.9 ms,
+# bench neutral (profiles/r6_sort/), so off by default.
+FUSED_GATHER = os.environ.get("LSKNN_FUSED_GATHER", "0") == "1"
+
+
 def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
                 keys: tuple | None = None, grid: bool = False, density_n: int | None = None,
                 grid_level: int | None = None, grid_gated: bool = True) -> LocalIndex:
@@ -159,17 +165,23 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     if box is None:
         box = K.bounds(points)
     gpu = K.is_gpu(points)
-    if keys is not None:  # (keys, None): values 0..n-1 generated by the sort
-        skeys, perm = (K.sort_pairs(keys[0], keys[1], 30) if keys[1] is not None
-                       else K.sort_keys_iota(keys[0], 30))
-    elif gpu:  # (the sort's first pass generates the values: no iota array)
-        skeys, perm = K.sort_keys_iota(K.morton(points, box, with_iota=False)[0], 30)
+    spts = None  # points in sorted order, gathered by the sort's last pass (FUSED_GATHER)
+    if keys is not None and keys[1] is not None:
+        skeys, perm = K.sort_pairs(keys[0], keys[1], 30)
+    elif gpu or keys is not None:  # (the sort's first pass generates the values: no iota array)
+        kk = keys[0] if keys is not None else K.morton(points, box, with_iota=False)[0]
+        if FUSED_GATHER and gpu and n >= 2:
+            skeys, perm, spts = K.sort_keys_iota_gather(kk, points, 30, pad=K.PAD_POINTS)
+        else:
+            skeys, perm = K.sort_keys_iota(kk, 30)
     else:
         skeys, perm = K.sort_pairs(*K.morton(points, box), 30)
     # level census (grid) and over-full-cell flag (refinement) in one pass over the keys
     census = K.key_census(skeys[:n], HEAVY_RUN) if gpu and n > 1 else None
+    sorted_perm = perm
     perm = refine_heavy_cells(points, skeys, perm, heavy=census[1] if census is not None else None)
-    pts = K.gather3(points, perm, pad=K.PAD_POINTS)
+    # (a refinement reorders over-full cells: the fused gather's order is then stale)
+    pts = spts if spts is not None and perm is sorted_perm else K.gather3(points, perm, pad=K.PAD_POINTS)
     nodes, qnodes, depth = K.build_tree(pts, n)
     index = LocalIndex(n, pts, perm, nodes, qnodes, depth, box)
     if grid:

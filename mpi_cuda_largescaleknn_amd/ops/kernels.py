@@ -141,6 +141,30 @@ def sort_keys_iota(keys: torch.Tensor, key_bits: int = 30):
     return (ka, va) if alt.value else (keys, vals)
 
 
+def sort_keys_iota_gather(keys: torch.Tensor, points: torch.Tensor, key_bits: int = 30, pad: int = 0):
+    """sort_keys_iota + the points in sorted order (`pad` extra zero rows), gathered by the
+    sort's last pass instead of a separate gather3 over the permutation. Returns (sorted
+    keys, permutation, sorted points)."""
+    n = keys.shape[0]
+    if not is_gpu(keys) or n < 2:
+        sk, perm = sort_keys_iota(keys, key_bits)
+        return sk, perm, gather3(points, perm, pad=pad)
+    lib = _native.hip()
+    vals = torch.empty_like(keys)
+    ka = torch.empty_like(keys)
+    va = torch.empty_like(keys)
+    ws = torch.empty(lib.lsk_hip_sort_ws_bytes(n), dtype=torch.uint8, device=keys.device)
+    pts = torch.empty((n + pad, 3), dtype=torch.float32, device=keys.device)
+    if pad:
+        pts[n:].zero_()
+    points = points.contiguous()
+    alt = C.c_int(0)
+    check(lib.lsk_hip_sort_keys_iota_gather(_ptr(keys), _ptr(vals), _ptr(ka), _ptr(va), n, key_bits, _ptr(ws),
+                                            C.byref(alt), _ptr(points), _ptr(pts), _stream(keys)),
+          "sort_keys_iota_gather")
+    return ((ka, va) if alt.value else (keys, vals)) + (pts,)
+
+
 def key_census(skeys: torch.Tensor, run: int) -> tuple[torch.Tensor, torch.Tensor]:
     """One device pass over sorted keys: (int64 [11] level counts as key_levels_dev, int32
     [1] heavy flag: some key equals the one `run` positions earlier). No host read."""

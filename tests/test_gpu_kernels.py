@@ -73,6 +73,32 @@ def test_sort_keys_iota_equals_sort_pairs(n, bits):
     assert torch.equal(ks.cpu(), kr) and torch.equal(vs.cpu(), vr)
 
 
+@pytest.mark.parametrize("n", [1, 2, 4097, 1000003])
+@pytest.mark.parametrize("bits", [8, 30])
+def test_sort_keys_iota_gather_equals_sort_then_gather(n, bits):
+    """The point gather fused into the sort's last pass (sort_keys_iota_gather, behind
+    LSKNN_FUSED_GATHER): the same keys and permutation, the points in that order, the
+    padding rows zero — and build_index with it on equals build_index with it off."""
+    g = torch.Generator().manual_seed(n * 3 + bits)
+    keys = torch.randint(0, 1 << bits, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    pts = torch.rand((n, 3), generator=g).to(DEV)
+    ks, vs, sp = K.sort_keys_iota_gather(keys.to(DEV).clone(), pts, bits, pad=7)
+    kr, vr = K.sort_keys_iota(keys.to(DEV).clone(), bits)
+    assert torch.equal(ks.cpu(), kr.cpu()) and torch.equal(vs.cpu(), vr.cpu())
+    assert torch.equal(sp[:n].cpu(), pts.cpu()[vr.long().cpu()])
+    assert torch.equal(sp[n:].cpu(), torch.zeros(7, 3))
+
+
+def test_build_index_fused_gather_same_index(monkeypatch):
+    p = uniform(200_003, seed=9).to(DEV)
+    monkeypatch.setattr(E, "FUSED_GATHER", False)
+    a = E.build_index(p, grid=True)
+    monkeypatch.setattr(E, "FUSED_GATHER", True)
+    b = E.build_index(p, grid=True)
+    assert torch.equal(a.pts.cpu(), b.pts.cpu()) and torch.equal(a.perm.cpu(), b.perm.cpu())
+    assert torch.equal(a.nodes.cpu(), b.nodes.cpu()) and torch.equal(a.grid.slots.cpu(), b.grid.slots.cpu())
+
+
 @pytest.mark.parametrize("heavy", [False, True])
 def test_key_census_counts_and_heavy_flag(heavy):
     """key_census = key_levels + the over-full-cell flag of refine_heavy_cells, one pass."""
