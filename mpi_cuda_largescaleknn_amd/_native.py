@@ -58,7 +58,7 @@ class TreeView(C.Structure):
     ]
 
 
-HIP_ABI = 9  # lsk_hip_abi_version() of a library matching the structs below
+HIP_ABI = 10  # lsk_hip_abi_version() of a library matching the structs below
 
 
 class KnnArgs(C.Structure):
@@ -90,6 +90,7 @@ class KnnArgs(C.Structure):
         ("pad2", C.c_int32),
         ("ngroups_dev", vp),
         ("wq", vp),
+        ("qrot", vp),
     ]
 
 

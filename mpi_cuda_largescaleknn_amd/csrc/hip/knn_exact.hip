@@ -62,13 +62,15 @@ __device__ __forceinline__ uint32_t cand_bits(float qx, float qy, float qz, cons
 
 // Histogram every value v in [lo, hi) of the points of buckets [b0, b1) of one tree into
 // hist[(v-lo)>>shift].
-__device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz, uint32_t lo,
-                           uint32_t hi, uint32_t shift, uint32_t *hist, uint32_t *stk, int64_t b0,
+// (bx, by, bz): the query in the tree's frame for the box tests (= qx.. unless the tree was
+// built in a rotated frame, lsk_knn_args.qrot); distances use qx..
+__device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz, float bx, float by, float bz,
+                           uint32_t lo, uint32_t hi, uint32_t shift, uint32_t *hist, uint32_t *stk, int64_t b0,
                            int64_t b1, int lane) {
   if (T.n <= 0 || b0 >= b1) return;
   const int32_t depth = T.depth;
   const float lim = bitsf(hi);  // a box at distance >= bitsf(hi) holds no value < hi
-  const lsk::vec3f q{qx, qy, qz};
+  const lsk::vec3f q{bx, by, bz};
   const float4 *nodes = (const float4 *)T.nodes;
   uint32_t sp = 1;
   if (lane == 0) stk[0] = 1u;
@@ -113,9 +115,9 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
       if (need) {
         // farthest corner (per-axis float differences, squares and fma are monotone: no
         // point inside is farther)
-        const float fx = fmaxf(fabsf(lo4.x - qx), fabsf(hi4.x - qx));
-        const float fy = fmaxf(fabsf(lo4.y - qy), fabsf(hi4.y - qy));
-        const float fz = fmaxf(fabsf(lo4.z - qz), fabsf(hi4.z - qz));
+        const float fx = fmaxf(fabsf(lo4.x - bx), fabsf(hi4.x - bx));
+        const float fy = fmaxf(fabsf(lo4.y - by), fabsf(hi4.y - by));
+        const float fz = fmaxf(fabsf(lo4.z - bz), fabsf(hi4.z - bz));
         const uint32_t fb = fbits(lsk::dist2(fx, fy, fz)), nb = fbits(nd);
         if (fb < lo) {
           // shell test: only values below lo, counted by the previous passes
@@ -165,6 +167,9 @@ __device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds<W> &L,
   const float qx = lsk::uniform_f(A.qpts[3 * qi]);
   const float qy = lsk::uniform_f(A.qpts[3 * qi + 1]);
   const float qz = lsk::uniform_f(A.qpts[3 * qi + 2]);
+  const float bx = A.qrot ? lsk::uniform_f(A.qrot[3 * qi]) : qx;
+  const float by = A.qrot ? lsk::uniform_f(A.qrot[3 * qi + 1]) : qy;
+  const float bz = A.qrot ? lsk::uniform_f(A.qrot[3 * qi + 2]) : qz;
   const uint32_t cut_b = (A.cut2 == A.cut2) ? fbits(fmaxf(A.cut2, 0.f)) : lsk::kInfBits;
   const uint32_t cut_lim = cut_b < lsk::kInfBits ? cut_b : lsk::kInfBits;
   int64_t total = 0;
@@ -198,7 +203,7 @@ __device__ uint32_t exact_kth(const lsk_knn_args &A, int64_t qi, ExactLds<W> &L,
     qbarrier<W>();
     for (int t = 0; t < A.ntrees; t++) {
       const int64_t nb = (A.tree[t].n + lsk::kBucket - 1) / lsk::kBucket;
-      count_tree(A.tree[t], qx, qy, qz, lo, hi, shift, L.hist, L.stk[wq], nb * wq / W, nb * (wq + 1) / W,
+      count_tree(A.tree[t], qx, qy, qz, bx, by, bz, lo, hi, shift, L.hist, L.stk[wq], nb * wq / W, nb * (wq + 1) / W,
                  lane);
     }
     qbarrier<W>();

@@ -163,7 +163,8 @@ struct WaveLdsR {
 };
 
 struct Lane {
-  float qx, qy, qz;
+  float qx, qy, qz;  // the query (NT == 3: in the trees' rotated frame, for the box tests)
+  float ox, oy, oz;  // NT == 3 only: the query's own coordinates (the canonical distances)
   uint32_t state;
   uint32_t lo_b, hi_b, shift;  // histogram range; lo_b = the answer once DONE
   int32_t bin_hi;
@@ -296,9 +297,12 @@ __device__ __forceinline__ float rowb(float v) {
 
 // Candidate J of the row's quarter (padding lanes hold +inf coordinates: d² = inf,
 // which is above every histogram range and collect band).
-template <int J>
+// NT: tree count of the kernel instance; 3 = one tree built in a rotated frame (the query's
+// own coordinates are then s.ox.., s.qx.. being the rotated ones its box tests use).
+template <int J, int NT>
 __device__ __forceinline__ uint32_t cand(const Lane &s, float px, float py, float pz) {
-  const float d2 = lsk::dist2(s.qx - rowb<J>(px), s.qy - rowb<J>(py), s.qz - rowb<J>(pz));
+  const float qx = NT == 3 ? s.ox : s.qx, qy = NT == 3 ? s.oy : s.qy, qz = NT == 3 ? s.oz : s.qz;
+  const float d2 = lsk::dist2(qx - rowb<J>(px), qy - rowb<J>(py), qz - rowb<J>(pz));
   return fbits(d2);
 }
 
@@ -354,30 +358,30 @@ __device__ __forceinline__ bool update8(Lane &s, const uint32_t (&u)[G], uint32_
 }
 
 // The 16 candidates of this lane's row quarter (lane i of the row holds candidate i).
-template <int MODE>
+template <int MODE, int NT>
 __device__ __forceinline__ bool process16(Lane &s, float px, float py, float pz, uint32_t cnt,
                                           uint32_t *pool, int lane, uint32_t trash, uint32_t k, bool &crowd) {
   bool lane_in;
   // groups of 4 candidates: 4 fewer live VGPRs in the hot loop than groups of 8
   {
-    uint32_t u[4] = {cand<0>(s, px, py, pz), cand<1>(s, px, py, pz), cand<2>(s, px, py, pz),
-                     cand<3>(s, px, py, pz)};
+    uint32_t u[4] = {cand<0, NT>(s, px, py, pz), cand<1, NT>(s, px, py, pz), cand<2, NT>(s, px, py, pz),
+                     cand<3, NT>(s, px, py, pz)};
     lane_in = update8<MODE, 4>(s, u, pool, lane, trash);
   }
   {
-    uint32_t u[4] = {cand<4>(s, px, py, pz), cand<5>(s, px, py, pz), cand<6>(s, px, py, pz),
-                     cand<7>(s, px, py, pz)};
+    uint32_t u[4] = {cand<4, NT>(s, px, py, pz), cand<5, NT>(s, px, py, pz), cand<6, NT>(s, px, py, pz),
+                     cand<7, NT>(s, px, py, pz)};
     lane_in = update8<MODE, 4>(s, u, pool, lane, trash) || lane_in;
   }
   if (__ballot(cnt > 8u)) {
     {
-      uint32_t u[4] = {cand<8>(s, px, py, pz), cand<9>(s, px, py, pz), cand<10>(s, px, py, pz),
-                       cand<11>(s, px, py, pz)};
+      uint32_t u[4] = {cand<8, NT>(s, px, py, pz), cand<9, NT>(s, px, py, pz), cand<10, NT>(s, px, py, pz),
+                       cand<11, NT>(s, px, py, pz)};
       lane_in = update8<MODE, 4>(s, u, pool, lane, trash) || lane_in;
     }
     {
-      uint32_t u[4] = {cand<12>(s, px, py, pz), cand<13>(s, px, py, pz), cand<14>(s, px, py, pz),
-                       cand<15>(s, px, py, pz)};
+      uint32_t u[4] = {cand<12, NT>(s, px, py, pz), cand<13, NT>(s, px, py, pz), cand<14, NT>(s, px, py, pz),
+                       cand<15, NT>(s, px, py, pz)};
       lane_in = update8<MODE, 4>(s, u, pool, lane, trash) || lane_in;
     }
   }
@@ -444,18 +448,19 @@ __device__ __forceinline__ lsk_tree_view pick_tree(const lsk_knn_args &A, uint32
 // Branch-free (the load is always issued, from a clamped in-bounds address), so the
 // compiler can count outstanding loads and the prefetch is not serialised by vmcnt(0).
 // 32-bit index math (trees hold < 2^31 points, checked on the host).
-// NT = number of trees the kernel instance handles (1: no per-lane tree selects).
+// NT = number of trees the kernel instance handles (1: no per-lane tree selects; 3: one
+// tree in a rotated frame).
 template <int NT>
 __device__ __forceinline__ uint32_t load_quarter(const WaveCtx &W, uint32_t e, float &px, float &py,
                                                  float &pz) {
   const bool ok = e != kInvalid;
-  const bool t1 = NT > 1 && (e >> 31) != 0;
+  const bool t1 = NT == 2 && (e >> 31) != 0;
   const uint32_t n = t1 ? W.n1 : W.n0;
   const uint32_t q16 = (e & 0x7fffffffu) << 4;
   const uint32_t idx = q16 | (uint32_t)(W.lane & 15);
   const bool live = ok && idx < n;
   // dead lanes read point 0 of a non-empty tree
-  const float *p = NT == 1 ? W.p0 + 3u * (live ? idx : 0u)
+  const float *p = NT != 2 ? W.p0 + 3u * (live ? idx : 0u)
                            : (live ? (t1 ? W.p1 : W.p0) + 3u * idx : W.pdef);
   px = p[0];  // raw: the consumer substitutes +inf for padding lanes (see process_steps)
   py = p[1];
@@ -499,7 +504,7 @@ __device__ __forceinline__ void process_steps(Lane &s, WaveCtx &W, const lsk_knn
 #ifdef LSK_PROFILE
     s.pband = false;
 #endif
-    const bool lin = process16<MODE>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.trash, W.k, W.crowd);
+    const bool lin = process16<MODE, NT>(s, cx, cy, cz, ccnt, W.L->pool, W.lane, W.trash, W.k, W.crowd);
     if (W.steps >= max(kStepBudget, kStepsPerK * W.k)) W.guard |= 2u;
 #ifdef LSK_PROFILE
     if (MODE == MODE_HIST) {
@@ -1120,8 +1125,10 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
     lsk::set_last_error("knn_rows: k must be in [1, 65535] for the radix-select kernel");
     return 1;
   }
-  if (A.nq >= ((int64_t)1 << 32) || A.ntrees < 0 || A.ntrees > 2 || A.seed < 0 || A.seed > 64) {
-    lsk::set_last_error("knn_rows: nq must be < 2^32, ntrees in [0,2], seed in [0,64]");
+  if (A.nq >= ((int64_t)1 << 32) || A.ntrees < 0 || A.ntrees > 2 || A.seed < 0 || A.seed > 64 ||
+      (A.qrot && A.ntrees != 1)) {
+    lsk::set_last_error("knn_rows: nq must be < 2^32, ntrees in [0,2], seed in [0,64]; a rotated frame "
+                        "(qrot) with one tree");
     return 1;
   }
   for (int t = 0; t < A.ntrees; t++) {
@@ -1144,10 +1151,14 @@ extern "C" int lsk_hip_knn_rows(const lsk_knn_args *args, void *stream) {
     const unsigned sblk = nblk < cap ? nblk : cap;
     if (A.ntrees > 1)
       knn_rows_kernel<LSK_RCAP, 2, true><<<sblk, kThreads, 0, st>>>(A);
+    else if (A.qrot)
+      knn_rows_kernel<LSK_RCAP, 3, true><<<sblk, kThreads, 0, st>>>(A);
     else
       knn_rows_kernel<LSK_RCAP, 1, true><<<sblk, kThreads, 0, st>>>(A);
   } else if (A.ntrees > 1) {
     knn_rows_kernel<LSK_RCAP, 2, false><<<nblk, kThreads, 0, st>>>(A);
+  } else if (A.qrot) {
+    knn_rows_kernel<LSK_RCAP, 3, false><<<nblk, kThreads, 0, st>>>(A);
   } else {
     knn_rows_kernel<LSK_RCAP, 1, false><<<nblk, kThreads, 0, st>>>(A);
   }

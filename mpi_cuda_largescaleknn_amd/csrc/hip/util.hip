@@ -17,7 +17,7 @@ void set_last_error(const std::string &msg) {
 }
 }  // namespace lsk
 
-extern "C" int lsk_hip_abi_version(void) { return 9; }
+extern "C" int lsk_hip_abi_version(void) { return 10; }
 
 extern "C" const char *lsk_hip_last_error(void) {
   static thread_local std::string copy;

@@ -112,6 +112,8 @@ class LocalIndex:
     depth: int
     box: torch.Tensor        # [8] cube used for the curve keys
     grid: GridIndex | None = None
+    qrot: torch.Tensor | None = None  # [n + PAD, 3]: the sorted points in the rotated frame the
+                                      # keys, tree boxes and box tests use (flat_frame), or None
 
     @property
     def device(self) -> torch.device:
@@ -148,9 +150,88 @@ class KnnStats:
 FUSED_GATHER = os.environ.get("LSKNN_FUSED_GATHER", "0") == "1"
 
 
+# Flat data in any orientation (a tilted plane, a slanted line): the bucket tree's axis-
+# aligned boxes around a slanted patch are as thick as they are wide, so they cull like 3-D
+# boxes around 2-D data (2e7 points, k = 100: tilted plane 649.6 vs axis-aligned plane
+# 1239.0 Mpts/s). flat_frame finds the principal axes of such a set; build_index then sorts
+# and boxes the points in that frame (keys, tree boxes, box tests) while every distance stays
+# canonical in the points' own coordinates, so outputs are bit-identical. The boxes are
+# widened by a bound on the rotation's rounding (rotate_margin): culling stays conservative.
+# 0: off (A/B).
+FLAT_FRAME = os.environ.get("LSKNN_FLAT_FRAME", "1") != "0"
+FLAT_RATIO = 1e-6        # smallest / largest principal variance of a flat set
+FRAME_SAMPLE = 1 << 13   # points sampled for the covariance (strided)
+
+
+class FrameProbe:
+    """The flatness test of flat_frame without a host wait up front: a strided sample's
+    3x3 covariance is computed on the device (float64 sums) and copied to pinned memory
+    behind an event; result() reads it later (the unrotated index is built meanwhile) and
+    returns the rotation, or None."""
+
+    def __init__(self, points: torch.Tensor):
+        self.cov = None
+        n = points.shape[0]
+        if not FLAT_FRAME or not K.is_gpu(points) or n < 1024 or _SYNC_FREE[0] \
+                or torch.cuda.is_current_stream_capturing():
+            return
+        smp = points[::max(1, n // FRAME_SAMPLE)][:FRAME_SAMPLE].to(torch.float64)
+        c = smp - smp.mean(0)
+        v = torch.stack([(c[:, i] * c[:, j]).sum() for i, j in ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2))])
+        self.cov = torch.empty(6, dtype=torch.float64, pin_memory=True)
+        self.cov.copy_(v, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        self.device = points.device
+
+    def result(self) -> torch.Tensor | None:
+        if self.cov is None:
+            return None
+        self.ev.synchronize()
+        a = self.cov.numpy()
+        cov = np.array([[a[0], a[1], a[2]], [a[1], a[3], a[4]], [a[2], a[4], a[5]]])
+        if not np.isfinite(cov).all():
+            return None
+        w, v = np.linalg.eigh(cov)  # ascending
+        # a plane: one principal variance negligible, the other two not (a line is served
+        # better in its own frame: rotated, 2e7 points took 191 vs 706 Mpts/s)
+        if not (w[2] > 0) or w[0] > FLAT_RATIO * w[2] or w[1] < 1e-3 * w[2]:
+            return None
+        if np.max(np.abs(v[:, 0])) > 1.0 - 1e-6:  # already axis-aligned: the tree is thin as is
+            return None
+        R = v[:, ::-1].T.copy()  # rows: axes by decreasing variance
+        return torch.tensor(R, dtype=torch.float32, device=self.device)
+
+
+def flat_frame(points: torch.Tensor) -> torch.Tensor | None:
+    """3x3 float32 rotation (rows: principal axes, largest variance first) when `points`
+    (GPU) lie on a plane that is not already aligned with the coordinate axes, else None
+    (FrameProbe, read at once; eager paths only: never inside a HIP-graph capture or a
+    stream of sets)."""
+    return FrameProbe(points).result()
+
+
+def rotate(points: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
+    """points @ R^T with explicit fp32 multiply-adds (no reduced-precision GEMM path)."""
+    p0, p1, p2 = points[:, 0:1], points[:, 1:2], points[:, 2:3]
+    return p0 * R[:, 0] + p1 * R[:, 1] + p2 * R[:, 2]
+
+
+def rotate_margin(rbox: torch.Tensor) -> torch.Tensor:
+    """Per-side widening of every box built from rotated points (device scalar): bounds the
+    difference between distances in the rotated frame (float-evaluated, non-orthonormal
+    float matrix) and the canonical float distances in the points' own frame — ~9 ulp of the
+    largest coordinate for the rotation, a few ulp of the extent for the distances — with a
+    wide safety factor (2^-16 of |coordinate| + extent)."""
+    mag = torch.maximum(rbox[0:3].abs(), rbox[3:6].abs()).max()
+    ext = (rbox[3:6] - rbox[0:3]).max()
+    return (mag * 1.7320508 + ext) * (2.0 ** -16)
+
+
 def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
                 keys: tuple | None = None, grid: bool = False, density_n: int | None = None,
-                grid_level: int | None = None, grid_gated: bool = True) -> LocalIndex:
+                grid_level: int | None = None, grid_gated: bool = True,
+                frame: torch.Tensor | None = None) -> LocalIndex:
     """Sort points along the space-filling curve of `box` (default: their own bounds) and
     build the bucket tree. `keys` = (keys, iota) computed already (SetStream's PRE_KEYS:
     the next set's box and curve keys on the side stream beside the current k-NN). `grid`: also index the sorted points by the cell grid of
@@ -158,10 +239,14 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     fill `box` (a rank's share of a global box: the global count; default: n).
     `grid_level`: force the grid's grandchild level (tests; a halo index takes the local
     grid's); `grid_gated=False`: no census / device gate for the grid (build_grid).
+    `frame` (flat_frame, GPU, with no keys or box given): the index is built in that rotated
+    frame (no grid) — see FLAT_FRAME.
     No host read on the way unless an over-full key cell needs the eager refinement
     (refine_heavy_cells; under host_sync_free() not even that)."""
     points = points.contiguous()
     n = points.shape[0]
+    if frame is not None and K.is_gpu(points) and keys is None and box is None and n >= 2:
+        return _build_rotated(points, frame)
     if box is None:
         box = K.bounds(points)
     gpu = K.is_gpu(points)
@@ -188,6 +273,26 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
         index.grid = build_grid(index, skeys, density_n, grid_level,
                                 counts=census[0] if census is not None else None, gated=grid_gated)
     return index
+
+
+def _build_rotated(points: torch.Tensor, R: torch.Tensor) -> LocalIndex:
+    """build_index in the frame R: curve keys, sort and tree boxes from the rotated points
+    (boxes widened by rotate_margin), the index's points (the candidates' coordinates) in
+    their own frame, qrot the queries in the rotated one. No grid (flat data)."""
+    n = points.shape[0]
+    rp = rotate(points, R).contiguous()
+    rbox = K.bounds(rp)
+    skeys, perm = K.sort_keys_iota(K.morton(rp, rbox, with_iota=False)[0], 30)
+    census = K.key_census(skeys[:n], HEAVY_RUN) if n > 1 else None
+    perm = refine_heavy_cells(rp, skeys, perm, heavy=census[1] if census is not None else None)
+    pts = K.gather3(points, perm, pad=K.PAD_POINTS)
+    qrot = K.gather3(rp, perm, pad=K.PAD_POINTS)
+    nodes, qnodes, depth = K.build_tree(qrot, n)
+    m = rotate_margin(rbox)
+    for t in (nodes, qnodes):
+        t[:, 0:3] -= m
+        t[:, 4:7] += m
+    return LocalIndex(n, pts, perm, nodes, qnodes, depth, rbox, qrot=qrot)
 
 
 def grid_level_for(density_n: int, n_local: int, ms: float = GRID_MS) -> int:
@@ -521,10 +626,13 @@ def query(index: LocalIndex, cfg: KnnConfig, hint2: float | torch.Tensor = 0.0, 
     trees = [index.tree()] + ([extra.tree()] if extra is not None and extra.n > 0 else [])
     raw = torch.zeros(32, dtype=torch.int64, device=index.device) if stats is not None else None
     kw = dict(groups=groups, ngroups=ngroups, seed=SEED_BUCKETS, init_d2=init_d2,
-              out_perm=index.perm if final_out is not None else None, out_final=final_out)
+              out_perm=index.perm if final_out is not None else None, out_final=final_out,
+              qrot=index.qrot if len(trees) == 1 else None)
     impl = KNN_IMPL
     # two grids: the halo re-query of a distributed run (the halo index has a grid of its
     # own, pipelines._halo_requery); the local index's gate still picks grid or rows
+    if index.qrot is not None and len(trees) != 1:
+        raise ValueError("query: an index built in a rotated frame serves its own points only (no extra tree)")
     two_grid = (impl == "rows" and index.grid is not None and len(trees) == 2 and extra.grid is not None
                 and cfg.k <= K.ROWS_MAX_K)
     use_grid = two_grid or (impl == "rows" and index.grid is not None and len(trees) == 1
@@ -629,7 +737,11 @@ def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,
     """Distance from every point to its k-th nearest neighbour among `points`
     (itself counted), in input order — the single-rank reference output."""
     cfg = KnnConfig(k=k, max_radius=max_radius)
+    probe = FrameProbe(points)  # (read after the build: no host wait before it)
     index = build_index(points, grid=True)
+    frame = probe.result()
+    if frame is not None:  # a tilted plane: rebuilt in its principal-axes frame
+        index = build_index(points, frame=frame)
     hint2 = radius_hint(index.box, index.n, k)
     out = torch.empty(index.n, dtype=torch.float32, device=points.device)
     return query(index, cfg, hint2, stats=stats, final_out=out)

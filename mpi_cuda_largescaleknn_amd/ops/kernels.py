@@ -354,7 +354,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
             seed: int = 0, impl: str = "rows", init_d2: torch.Tensor | None = None,
             out_perm: torch.Tensor | None = None, out_final: torch.Tensor | None = None,
             debug_fail_mod: int = 0, grid=None, ngroups_dev: torch.Tensor | None = None,
-            expect_grid: bool = True, short_list: bool = False, chunks: int = 1, grid2=None) -> FailWord:
+            expect_grid: bool = True, short_list: bool = False, chunks: int = 1, grid2=None,
+            qrot: torch.Tensor | None = None) -> FailWord:
     """k-th squared distance for sorted queries against up to two bucket trees.
 
     trees: list of (sorted_pts_padded, nodes, qnodes, n, depth). impl: "rows" (the
@@ -387,6 +388,8 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     kernel runs iff gate == 1 and knn_rows iff gate == 0.
     grid2 (impl "grid", two trees: the halo re-query): the second tree's grid (slots, level,
     box, inf4) — knn_grid2 walks both grids; init_d2 is allowed then.
+    qrot (one tree, rows / exact): the queries in the rotated frame trees[0]'s boxes were
+    built in (knn_engine.flat_frame); box tests use it, distances qpts.
     Returns the launch's FailWord.
     """
     if (out_perm is None) != (out_final is None):
@@ -422,6 +425,9 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.qstatus = _ptr(qstatus)
     a.seed = seed
     a.init_d2 = _ptr(init_d2)
+    if qrot is not None and (impl == "grid" or len(trees) != 1):
+        raise ValueError("knn_gpu: qrot needs one tree and the rows / exact kernel")
+    a.qrot = _ptr(qrot)
     a.out_perm = _ptr(out_perm)
     a.out_final = _ptr(out_final)
     a.debug_fail_mod = int(debug_fail_mod)

@@ -96,7 +96,8 @@ def test_build_index_fused_gather_same_index(monkeypatch):
     monkeypatch.setattr(E, "FUSED_GATHER", True)
     b = E.build_index(p, grid=True)
     assert torch.equal(a.pts.cpu(), b.pts.cpu()) and torch.equal(a.perm.cpu(), b.perm.cpu())
-    assert torch.equal(a.nodes.cpu(), b.nodes.cpu()) and torch.equal(a.grid.slots.cpu(), b.grid.slots.cpu())
+    # (node 0 is unused: its slots are not written by the build)
+    assert torch.equal(a.nodes[1:].cpu(), b.nodes[1:].cpu()) and torch.equal(a.grid.slots.cpu(), b.grid.slots.cpu())
 
 
 @pytest.mark.parametrize("heavy", [False, True])
