@@ -161,6 +161,12 @@ FUSED_GATHER = os.environ.get("LSKNN_FUSED_GATHER", "0") == "1"
 FLAT_FRAME = os.environ.get("LSKNN_FLAT_FRAME", "1") != "0"
 FLAT_RATIO = 1e-6        # smallest / largest principal variance of a flat set
 FRAME_SAMPLE = 1 << 13   # points sampled for the covariance (strided)
+# The frame pays from k ~ 48 (2e7 tilted plane, k = 100: 647 -> 1012 Mpts/s; k = 16: 1485 ->
+# 1366, the rotated build's extra passes outweigh its cheaper walk); the probe is then read
+# before the build (FRAME_EARLY: non-flat data pay a ~1 % host wait; read after the build
+# instead, a plane pays a wasted build: 911 vs 1012). profiles/r6_nonuniform/flat_frame_ab.txt
+FRAME_MIN_K = 48
+FRAME_EARLY = os.environ.get("LSKNN_FRAME_EARLY", "1") == "1"
 
 
 class FrameProbe:
@@ -169,10 +175,10 @@ class FrameProbe:
     behind an event; result() reads it later (the unrotated index is built meanwhile) and
     returns the rotation, or None."""
 
-    def __init__(self, points: torch.Tensor):
+    def __init__(self, points: torch.Tensor, k: int = FRAME_MIN_K):
         self.cov = None
         n = points.shape[0]
-        if not FLAT_FRAME or not K.is_gpu(points) or n < 1024 or _SYNC_FREE[0] \
+        if not FLAT_FRAME or k < FRAME_MIN_K or not K.is_gpu(points) or n < 1024 or _SYNC_FREE[0] \
                 or torch.cuda.is_current_stream_capturing():
             return
         smp = points[::max(1, n // FRAME_SAMPLE)][:FRAME_SAMPLE].to(torch.float64)
@@ -737,11 +743,15 @@ def knn_distances(points: torch.Tensor, k: int, max_radius: float = math.inf,
     """Distance from every point to its k-th nearest neighbour among `points`
     (itself counted), in input order — the single-rank reference output."""
     cfg = KnnConfig(k=k, max_radius=max_radius)
-    probe = FrameProbe(points)  # (read after the build: no host wait before it)
-    index = build_index(points, grid=True)
-    frame = probe.result()
-    if frame is not None:  # a tilted plane: rebuilt in its principal-axes frame
-        index = build_index(points, frame=frame)
+    probe = FrameProbe(points, k)
+    if FRAME_EARLY:  # the probe read before the build (a short host wait, no wasted build)
+        frame = probe.result()
+        index = build_index(points, grid=frame is None, frame=frame)
+    else:  # read after the unrotated build: no host wait before it
+        index = build_index(points, grid=True)
+        frame = probe.result()
+        if frame is not None:  # a tilted plane: rebuilt in its principal-axes frame
+            index = build_index(points, frame=frame)
     hint2 = radius_hint(index.box, index.n, k)
     out = torch.empty(index.n, dtype=torch.float32, device=points.device)
     return query(index, cfg, hint2, stats=stats, final_out=out)

@@ -744,11 +744,12 @@ def local_build(points: torch.Tensor, comm: Comm, cfg: E.KnnConfig, n_total: int
     info.counts["owned_points"] = n_local
     # a flat set in any orientation: the index in its principal-axes frame (eager runs only:
     # flat_frame reads a 3x3 covariance; never in a stream of sets or a graph capture)
-    probe = E.FrameProbe(points) if pre is None and not comm.distributed and n_local == n_total else None
-    index = E.build_index(points, box, keys=keys, grid=True, density_n=n_total)
+    probe = E.FrameProbe(points, cfg.k) if pre is None and not comm.distributed and n_local == n_total else None
     frame = probe.result() if probe is not None else None
-    if frame is not None:  # a tilted plane: rebuilt in its principal-axes frame
+    if frame is not None:  # a tilted plane: indexed in its principal-axes frame
         index = E.build_index(points, frame=frame)
+    else:
+        index = E.build_index(points, box, keys=keys, grid=True, density_n=n_total)
     info.timer.mark("build")
     return index, hint2
 

@@ -8,9 +8,10 @@ if [ -z "$NOTEST" ]; then
   grep -q " passed" gpurun_out/r6ff_tests.log && ! grep -q " failed" gpurun_out/r6ff_tests.log || { echo "STOP: tests failed"; exit 5; }
 fi
 export LSK_DISTS=${LSK_DISTS:-tilted_plane,line,planar,clustered,duplicates,mixed_scale}
-for r in 1 2; do for f in 1 0; do
-  run 300 r6ff_${f}_$r.log env LSKNN_FLAT_FRAME=$f python -u scripts/dist_robustness.py 2e7 100 16 || exit $?
+for r in 1 2; do for f in 1 0 e; do
+  if [ $f = e ]; then ENVS="LSKNN_FLAT_FRAME=1 LSKNN_FRAME_EARLY=1"; else ENVS="LSKNN_FLAT_FRAME=$f"; fi
+  run 300 r6ff_${f}_$r.log env $ENVS python -u scripts/dist_robustness.py 2e7 100 16 || exit $?
 done; done
-for f in gpurun_out/r6ff_[01]_*.log; do echo "== $(basename $f)"; grep -h "^{'dist'" $f | python3 -c "
+for f in gpurun_out/r6ff_[01e]_*.log; do echo "== $(basename $f)"; grep -h "^{'dist'" $f | python3 -c "
 import sys, ast
 print('  ' + '  '.join(f\"{d['dist']}/{d['k']} {d['Mpts_s']} ({d['exact']})\" for d in map(ast.literal_eval, sys.stdin)))"; done

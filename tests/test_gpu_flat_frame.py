@@ -34,6 +34,15 @@ def _random_plane(n, seed):
 def test_flat_sets_rotated_frame_exact(gen, k):
     p = _random_plane(120_000, 3) if gen == "random_plane" else GENERATORS[gen](120_000, seed=2)
     assert E.flat_frame(p.to(DEV)) is not None
+    old = E.FRAME_MIN_K
+    E.FRAME_MIN_K = 1  # (the rotated path for every k here)
+    try:
+        _check(p, k, gen)
+    finally:
+        E.FRAME_MIN_K = old
+
+
+def _check(p, k, gen):
     for r in (math.inf, 0.01):
         st = E.KnnStats()
         got = E.knn_distances(p.to(DEV), k, max_radius=r, stats=st).cpu()
