@@ -132,3 +132,19 @@ static inline unsigned lsk_blocks(int64_t n, int per_block, unsigned cap = 0) {
   if (cap && b > (int64_t)cap) b = cap;
   return (unsigned)b;
 }
+
+// Fill nwords 32-bit words with v by a kernel instead of hipMemsetAsync: memset nodes in a
+// captured HIP graph were seen not to re-run on later replays (ROCm 7.0: the 88-byte and
+// 4-byte ones of the level census, and the grid's slot table — tests/test_gpu_graph.py read
+// a stale table after a replay on other data); a kernel node always does.
+__global__ __launch_bounds__(256) static void lsk_fill32_kernel(uint32_t *__restrict__ p, uint32_t v,
+                                                                int64_t nwords) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += stride) p[i] = v;
+}
+
+static inline hipError_t lsk_fill32(void *p, uint32_t v, int64_t nwords, hipStream_t st) {
+  if (nwords <= 0) return hipSuccess;
+  lsk_fill32_kernel<<<lsk_blocks(nwords, 256 * 4, 4096), 256, 0, st>>>((uint32_t *)p, v, nwords);
+  return hipGetLastError();
+}

@@ -1313,7 +1313,7 @@ extern "C" int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorte
   }
   const size_t nslot = (size_t)64 << (3 * level);
   hipStream_t st = (hipStream_t)stream;
-  LSK_HIP(hipMemsetAsync(slots, 0, nslot * 16, st));
+  LSK_HIP(lsk_fill32(slots, 0u, (int64_t)nslot * 4, st));
   if (n <= 0) return 0;
   grid_build_kernel<<<lsk_blocks(n, 256), 256, 0, st>>>(sorted_pts, sorted_keys, n, box, (uint32_t)level + 2u,
                                                         (uint4 *)slots);
@@ -1323,7 +1323,7 @@ extern "C" int lsk_hip_grid_build(const float *sorted_pts, const uint32_t *sorte
 
 extern "C" int lsk_hip_key_levels(const uint32_t *keys, int64_t n, unsigned long long *counts, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  LSK_HIP(hipMemsetAsync(counts, 0, 11 * sizeof(unsigned long long), st));
+  LSK_HIP(lsk_fill32(counts, 0u, 22, st));
   if (n <= 1) return 0;
   key_levels_kernel<<<lsk_blocks(n, 256, kLevelsBlocks), 256, 0, st>>>(keys, n, counts, 0, nullptr);
   LSK_CHECK_LAUNCH("key_levels");

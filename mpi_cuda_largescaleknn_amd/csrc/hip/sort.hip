@@ -318,7 +318,7 @@ extern "C" int lsk_hip_sort_keys_iota(uint32_t *keys, uint32_t *vals, uint32_t *
                                       int64_t n, int key_bits, void *ws, int *result_in_alt, void *stream) {
   if (n == 1) {  // (no pass runs: the single value must still be written)
     hipStream_t s = (hipStream_t)stream;
-    LSK_HIP(hipMemsetAsync(vals, 0, sizeof(uint32_t), s));
+    LSK_HIP(lsk_fill32(vals, 0u, 1, s));
     *result_in_alt = 0;
     return 0;
   }

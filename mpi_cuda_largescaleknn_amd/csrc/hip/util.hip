@@ -463,8 +463,8 @@ extern "C" int lsk_hip_segment_bounds(const float *pts, const uint32_t *seg, int
                                       float *lo, float *hi, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   if (nseg <= 0) return 0;
-  LSK_HIP(hipMemsetAsync(lo, 0xff, (size_t)nseg * 3 * sizeof(float), s));
-  LSK_HIP(hipMemsetAsync(hi, 0x00, (size_t)nseg * 3 * sizeof(float), s));
+  LSK_HIP(lsk_fill32(lo, 0xffffffffu, nseg * 3, s));
+  LSK_HIP(lsk_fill32(hi, 0u, nseg * 3, s));
   if (m > 0) {
     segment_bounds_kernel<<<lsk_blocks(m, 256 * kSegPer, 8192), 256, 0, s>>>(
         pts, seg, m, (uint32_t *)lo, (uint32_t *)hi);

@@ -170,10 +170,9 @@ FRAME_EARLY = os.environ.get("LSKNN_FRAME_EARLY", "1") == "1"
 
 
 class FrameProbe:
-    """The flatness test of flat_frame without a host wait up front: a strided sample's
-    3x3 covariance is computed on the device (float64 sums) and copied to pinned memory
-    behind an event; result() reads it later (the unrotated index is built meanwhile) and
-    returns the rotation, or None."""
+    """The flatness test of flat_frame: a strided sample's 3x3 covariance is computed on
+    the device (float64 sums); result() reads it (one small host read) and returns the
+    rotation, or None."""
 
     def __init__(self, points: torch.Tensor, k: int = FRAME_MIN_K):
         self.cov = None
@@ -183,18 +182,16 @@ class FrameProbe:
             return
         smp = points[::max(1, n // FRAME_SAMPLE)][:FRAME_SAMPLE].to(torch.float64)
         c = smp - smp.mean(0)
-        v = torch.stack([(c[:, i] * c[:, j]).sum() for i, j in ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2))])
-        self.cov = torch.empty(6, dtype=torch.float64, pin_memory=True)
-        self.cov.copy_(v, non_blocking=True)
-        self.ev = torch.cuda.Event()
-        self.ev.record()
+        # (read by result() with one small blocking copy: the probe is read before the build
+        # anyway, FRAME_EARLY, so a pinned buffer + event saved nothing)
+        self.cov = torch.stack([(c[:, i] * c[:, j]).sum() for i, j in ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2),
+                                                                         (2, 2))])
         self.device = points.device
 
     def result(self) -> torch.Tensor | None:
         if self.cov is None:
             return None
-        self.ev.synchronize()
-        a = self.cov.numpy()
+        a = self.cov.cpu().numpy()
         cov = np.array([[a[0], a[1], a[2]], [a[1], a[3], a[4]], [a[2], a[4], a[5]]])
         if not np.isfinite(cov).all():
             return None
