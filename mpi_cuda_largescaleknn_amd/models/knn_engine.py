@@ -167,6 +167,11 @@ FRAME_SAMPLE = 1 << 13   # points sampled for the covariance (strided)
 # instead, a plane pays a wasted build: 911 vs 1012). profiles/r6_nonuniform/flat_frame_ab.txt
 FRAME_MIN_K = 48
 FRAME_EARLY = os.environ.get("LSKNN_FRAME_EARLY", "1") == "1"
+# ... and only while the plane's k-NN radius (sqrt(k * area / (pi * n))) is >= FRAME_RADIUS_X
+# times the boxes' widening (rotate_margin): denser planes lose to the margin (tilted plane,
+# k = 100: 2e7 (ratio ~29) 647 -> 1012 Mpts/s, 2e8 (~9) 629 -> 379, 5e8 (~6) 342 -> 166;
+# profiles/r6_nonuniform/plane_frame_scale.txt).
+FRAME_RADIUS_X = 16.0
 
 
 class FrameProbe:
@@ -176,16 +181,18 @@ class FrameProbe:
 
     def __init__(self, points: torch.Tensor, k: int = FRAME_MIN_K):
         self.cov = None
+        self.k = k
         n = points.shape[0]
         if not FLAT_FRAME or k < FRAME_MIN_K or not K.is_gpu(points) or n < 1024 or _SYNC_FREE[0] \
                 or torch.cuda.is_current_stream_capturing():
             return
         smp = points[::max(1, n // FRAME_SAMPLE)][:FRAME_SAMPLE].to(torch.float64)
+        self.n, self.m = n, smp.shape[0]
         c = smp - smp.mean(0)
         # (read by result() with one small blocking copy: the probe is read before the build
         # anyway, FRAME_EARLY, so a pinned buffer + event saved nothing)
         self.cov = torch.stack([(c[:, i] * c[:, j]).sum() for i, j in ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2),
-                                                                         (2, 2))])
+                                                                         (2, 2))] + [smp.abs().max()])
         self.device = points.device
 
     def result(self) -> torch.Tensor | None:
@@ -201,6 +208,11 @@ class FrameProbe:
         if not (w[2] > 0) or w[0] > FLAT_RATIO * w[2] or w[1] < 1e-3 * w[2]:
             return None
         if np.max(np.abs(v[:, 0])) > 1.0 - 1e-6:  # already axis-aligned: the tree is thin as is
+            return None
+        # the k-NN radius against rotate_margin (extents of a uniform spread: sqrt(12 var))
+        e1, e2 = math.sqrt(12.0 * w[1] / self.m), math.sqrt(12.0 * w[2] / self.m)
+        radius = math.sqrt(self.k * e1 * e2 / (math.pi * max(self.n, 1)))
+        if radius < FRAME_RADIUS_X * (a[6] * 1.7320508 + e2) * 2.0 ** -16:
             return None
         R = v[:, ::-1].T.copy()  # rows: axes by decreasing variance
         return torch.tensor(R, dtype=torch.float32, device=self.device)

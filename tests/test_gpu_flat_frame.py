@@ -84,3 +84,12 @@ def test_rotated_index_boxes_contain_rotated_points():
     q = idx.qrot[:n]
     b = torch.arange(n, device=DEV) // 64
     assert bool((q >= leaves[b, 0:3]).all()) and bool((q <= leaves[b, 4:7]).all())
+
+
+def test_dense_planes_keep_their_own_frame(monkeypatch):
+    """The frame is refused once the plane's k-NN radius nears the boxes' rotation margin
+    (FRAME_RADIUS_X: measured loss at 2e8 points, k = 100)."""
+    p = GENERATORS["tilted_plane"](50_000, seed=1).to(DEV)
+    assert E.flat_frame(p) is not None
+    monkeypatch.setattr(E, "FRAME_RADIUS_X", 1e4)
+    assert E.flat_frame(p) is None
