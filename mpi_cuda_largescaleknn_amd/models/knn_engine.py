@@ -165,13 +165,25 @@ FRAME_SAMPLE = 1 << 13   # points sampled for the covariance (strided)
 # 1366, the rotated build's extra passes outweigh its cheaper walk); the probe is then read
 # before the build (FRAME_EARLY: non-flat data pay a ~1 % host wait; read after the build
 # instead, a plane pays a wasted build: 911 vs 1012). profiles/r6_nonuniform/flat_frame_ab.txt
-FRAME_MIN_K = 48
+FRAME_MIN_K = int(os.environ.get("LSKNN_FRAME_MIN_K", "48"))
 FRAME_EARLY = os.environ.get("LSKNN_FRAME_EARLY", "1") == "1"
 # ... and only while the plane's k-NN radius (sqrt(k * area / (pi * n))) is >= FRAME_RADIUS_X
-# times the boxes' widening (rotate_margin): denser planes lose to the margin (tilted plane,
-# k = 100: 2e7 (ratio ~29) 647 -> 1012 Mpts/s, 2e8 (~9) 629 -> 379, 5e8 (~6) 342 -> 166;
-# profiles/r6_nonuniform/plane_frame_scale.txt).
-FRAME_RADIUS_X = 16.0
+# times the boxes' widening (rotate_margin); measured wins down to a ratio of ~4 (5e8, k = 48).
+FRAME_RADIUS_X = float(os.environ.get("LSKNN_FRAME_RADIUS_X", "2"))
+# Curve keys in the plane's frame: above PLANE_2D_MIN points, 2-D Morton keys of the two
+# in-plane coordinates, 15 bits each — 3-D keys spend a third of their 30 bits on the flat
+# axis: 1024^2 cells, ~200 points each at 2e8, wider than the k-NN radius (tilted plane,
+# k = 100, 3-D -> 2-D keys: 2e8 379 -> 878, 5e8 167 -> 856 Mpts/s; at 2e7 the 3-D Hilbert
+# keys' locality wins, 987 vs 880; profiles/r6_nonuniform/plane_frame_scale.txt). Above it,
+# axis-aligned planes take the frame too for the same keys, and every k does (2e8, frame vs
+# own: tilted 875 / 1227 vs 630 / 912 at k = 100 / 16, axis-aligned 884 / 1248 vs 649 / 897).
+# LSKNN_PLANE_KEYS: auto | 2d | 3d.
+PLANE_KEYS = os.environ.get("LSKNN_PLANE_KEYS", "auto")
+PLANE_2D_MIN = 1 << 26
+
+
+def _plane_2d(n: int) -> bool:
+    return PLANE_KEYS == "2d" or (PLANE_KEYS == "auto" and n > PLANE_2D_MIN)
 
 
 class FrameProbe:
@@ -183,7 +195,8 @@ class FrameProbe:
         self.cov = None
         self.k = k
         n = points.shape[0]
-        if not FLAT_FRAME or k < FRAME_MIN_K or not K.is_gpu(points) or n < 1024 or _SYNC_FREE[0] \
+        if not FLAT_FRAME or (k < FRAME_MIN_K and not _plane_2d(n)) or not K.is_gpu(points) or n < 1024 \
+                or _SYNC_FREE[0] \
                 or torch.cuda.is_current_stream_capturing():
             return
         smp = points[::max(1, n // FRAME_SAMPLE)][:FRAME_SAMPLE].to(torch.float64)
@@ -207,8 +220,8 @@ class FrameProbe:
         # better in its own frame: rotated, 2e7 points took 191 vs 706 Mpts/s)
         if not (w[2] > 0) or w[0] > FLAT_RATIO * w[2] or w[1] < 1e-3 * w[2]:
             return None
-        if np.max(np.abs(v[:, 0])) > 1.0 - 1e-6:  # already axis-aligned: the tree is thin as is
-            return None
+        if np.max(np.abs(v[:, 0])) > 1.0 - 1e-6 and not _plane_2d(self.n):
+            return None  # already axis-aligned: the tree is thin as is (3-D keys either way)
         # the k-NN radius against rotate_margin (extents of a uniform spread: sqrt(12 var))
         e1, e2 = math.sqrt(12.0 * w[1] / self.m), math.sqrt(12.0 * w[2] / self.m)
         radius = math.sqrt(self.k * e1 * e2 / (math.pi * max(self.n, 1)))
@@ -290,6 +303,23 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     return index
 
 
+def _spread15(v: torch.Tensor) -> torch.Tensor:
+    """The low 15 bits of int32 v moved to the even bit positions."""
+    v = (v | (v << 8)) & 0x00FF00FF
+    v = (v | (v << 4)) & 0x0F0F0F0F
+    v = (v | (v << 2)) & 0x33333333
+    return (v | (v << 1)) & 0x55555555
+
+
+def plane_keys(rp: torch.Tensor, rbox: torch.Tensor) -> torch.Tensor:
+    """30-bit 2-D Morton keys of rotated points by their first two coordinates (the plane's
+    own axes), 15 bits each over the square of the larger in-plane extent."""
+    s = float(1 << 15) / torch.maximum(rbox[3] - rbox[0], rbox[4] - rbox[1]).clamp_min(1e-30)
+    x = ((rp[:, 0] - rbox[0]) * s).clamp_(0.0, 32767.0).to(torch.int32)
+    y = ((rp[:, 1] - rbox[1]) * s).clamp_(0.0, 32767.0).to(torch.int32)
+    return _spread15(x) | (_spread15(y) << 1)
+
+
 def _build_rotated(points: torch.Tensor, R: torch.Tensor) -> LocalIndex:
     """build_index in the frame R: curve keys, sort and tree boxes from the rotated points
     (boxes widened by rotate_margin), the index's points (the candidates' coordinates) in
@@ -297,7 +327,8 @@ def _build_rotated(points: torch.Tensor, R: torch.Tensor) -> LocalIndex:
     n = points.shape[0]
     rp = rotate(points, R).contiguous()
     rbox = K.bounds(rp)
-    skeys, perm = K.sort_keys_iota(K.morton(rp, rbox, with_iota=False)[0], 30)
+    keys = plane_keys(rp, rbox) if _plane_2d(n) else K.morton(rp, rbox, with_iota=False)[0]
+    skeys, perm = K.sort_keys_iota(keys, 30)
     census = K.key_census(skeys[:n], HEAVY_RUN) if n > 1 else None
     perm = refine_heavy_cells(rp, skeys, perm, heavy=census[1] if census is not None else None)
     pts = K.gather3(points, perm, pad=K.PAD_POINTS)

@@ -29,9 +29,13 @@ def _random_plane(n, seed):
     return (uv[:, :1] * a + uv[:, 1:] * b + torch.tensor([3.0, -1.0, 0.5])).contiguous()
 
 
+@pytest.mark.parametrize("keys", ["3d", "2d"])
 @pytest.mark.parametrize("gen", ["tilted_plane", "random_plane"])
 @pytest.mark.parametrize("k", [1, 8, 100])
-def test_flat_sets_rotated_frame_exact(gen, k):
+def test_flat_sets_rotated_frame_exact(gen, k, keys, monkeypatch):
+    """3d: the curve keys of the rotated points; 2d: 2-D Morton keys of the in-plane axes
+    (the default above PLANE_2D_MIN points)."""
+    monkeypatch.setattr(E, "PLANE_KEYS", keys)
     p = _random_plane(120_000, 3) if gen == "random_plane" else GENERATORS[gen](120_000, seed=2)
     assert E.flat_frame(p.to(DEV)) is not None
     old = E.FRAME_MIN_K
@@ -93,3 +97,14 @@ def test_dense_planes_keep_their_own_frame(monkeypatch):
     assert E.flat_frame(p) is not None
     monkeypatch.setattr(E, "FRAME_RADIUS_X", 1e4)
     assert E.flat_frame(p) is None
+
+
+def test_axis_aligned_plane_takes_the_frame_with_2d_keys(monkeypatch):
+    """Above PLANE_2D_MIN an axis-aligned plane is indexed in its frame too (for the 2-D
+    keys); still bit-exact."""
+    p = GENERATORS["planar"](100_000, seed=3)
+    assert E.flat_frame(p.to(DEV)) is None
+    monkeypatch.setattr(E, "PLANE_2D_MIN", 50_000)
+    monkeypatch.setattr(E, "FRAME_MIN_K", 1)
+    assert E.flat_frame(p.to(DEV)) is not None
+    _check(p, 16, "planar")
