@@ -15,6 +15,7 @@ from __future__ import annotations
 import math
 import os
 from dataclasses import dataclass, field
+from typing import NamedTuple
 
 import numpy as np
 import torch
@@ -182,6 +183,26 @@ PLANE_KEYS = os.environ.get("LSKNN_PLANE_KEYS", "auto")
 PLANE_2D_MIN = 1 << 26
 
 
+# A line (two principal variances negligible) keeps its own frame (rotated fp32 coordinates
+# cannot resolve a dense line: profiles/r6_nonuniform/line_frame_ab.txt) but is sorted by its
+# position along the axis (line_keys) instead of 3-D curve keys. LSKNN_LINE_KEYS=0: off.
+LINE_KEYS = os.environ.get("LSKNN_LINE_KEYS", "1") != "0"
+
+
+class LineAxis(NamedTuple):
+    """FrameProbe's verdict for a line: its unit direction (float32 [3], device)."""
+    a: torch.Tensor
+
+
+def line_keys(points: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    """30-bit keys of points by their projection on the direction a (float32 arithmetic:
+    ~24 significant bits; ties in any order)."""
+    t = points[:, 0] * a[0] + points[:, 1] * a[1] + points[:, 2] * a[2]
+    lo, hi = t.min(), t.max()
+    t = (t - lo) * (float(1 << 30) / (hi - lo).clamp_min(1e-30))
+    return t.clamp_(0.0, float((1 << 30) - 64)).to(torch.int32)
+
+
 def _plane_2d(n: int) -> bool:
     return PLANE_KEYS == "2d" or (PLANE_KEYS == "auto" and n > PLANE_2D_MIN)
 
@@ -195,7 +216,7 @@ class FrameProbe:
         self.cov = None
         self.k = k
         n = points.shape[0]
-        if not FLAT_FRAME or (k < FRAME_MIN_K and not _plane_2d(n)) or not K.is_gpu(points) or n < 1024 \
+        if not FLAT_FRAME or (k < FRAME_MIN_K and not _plane_2d(n) and not LINE_KEYS) or not K.is_gpu(points) or n < 1024 \
                 or _SYNC_FREE[0] \
                 or torch.cuda.is_current_stream_capturing():
             return
@@ -216,9 +237,13 @@ class FrameProbe:
         if not np.isfinite(cov).all():
             return None
         w, v = np.linalg.eigh(cov)  # ascending
-        # a plane: one principal variance negligible, the other two not (a line is served
-        # better in its own frame: rotated, 2e7 points took 191 vs 706 Mpts/s)
-        if not (w[2] > 0) or w[0] > FLAT_RATIO * w[2] or w[1] < 1e-3 * w[2]:
+        if not (w[2] > 0) or w[0] > FLAT_RATIO * w[2]:
+            return None
+        if w[1] <= FLAT_RATIO * w[2]:  # a line: sorted along its axis, in its own frame
+            return LineAxis(torch.tensor(v[:, 2].copy(), dtype=torch.float32, device=self.device)) \
+                if LINE_KEYS else None
+        # a plane: one principal variance negligible, the other two not
+        if w[1] < 1e-3 * w[2] or (self.k < FRAME_MIN_K and not _plane_2d(self.n)):
             return None
         if np.max(np.abs(v[:, 0])) > 1.0 - 1e-6 and not _plane_2d(self.n):
             return None  # already axis-aligned: the tree is thin as is (3-D keys either way)
@@ -273,6 +298,10 @@ def build_index(points: torch.Tensor, box: torch.Tensor | None = None,
     (refine_heavy_cells; under host_sync_free() not even that)."""
     points = points.contiguous()
     n = points.shape[0]
+    if isinstance(frame, LineAxis):  # a line: its own frame, keys along its axis, no grid
+        if keys is None and K.is_gpu(points) and n >= 2:
+            keys, grid = (line_keys(points, frame.a), None), False
+        frame = None
     if frame is not None and K.is_gpu(points) and keys is None and box is None and n >= 2:
         return _build_rotated(points, frame)
     if box is None:

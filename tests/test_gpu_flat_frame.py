@@ -56,7 +56,7 @@ def _check(p, k, gen):
 def test_flat_frame_only_for_unaligned_planes():
     assert E.flat_frame(uniform(50_000, seed=1).to(DEV)) is None  # 3-D
     assert E.flat_frame(GENERATORS["planar"](50_000, seed=1).to(DEV)) is None  # axis-aligned plane
-    assert E.flat_frame(GENERATORS["line"](50_000, seed=1).to(DEV)) is None  # a line: not rotated
+    assert isinstance(E.flat_frame(GENERATORS["line"](50_000, seed=1).to(DEV)), E.LineAxis)  # not rotated
     assert E.flat_frame(GENERATORS["tilted_plane"](50_000, seed=1).to(DEV)) is not None
 
 
@@ -108,3 +108,33 @@ def test_axis_aligned_plane_takes_the_frame_with_2d_keys(monkeypatch):
     monkeypatch.setattr(E, "FRAME_MIN_K", 1)
     assert E.flat_frame(p.to(DEV)) is not None
     _check(p, 16, "planar")
+
+
+def _random_line(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.rand(n, generator=g) * 2 - 1
+    a = torch.tensor([-0.35, 0.8, 0.49])
+    return (t[:, None] * (a / a.norm()) + torch.tensor([1.5, 0.25, -2.0])).contiguous()
+
+
+def _axis_line(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.full((n, 3), 0.5)
+    p[:, 1] = torch.rand(n, generator=g)
+    return p
+
+
+@pytest.mark.parametrize("gen", ["line", "random_line", "axis_line"])
+@pytest.mark.parametrize("k", [1, 16, 100])
+def test_lines_sorted_along_their_axis_exact(gen, k):
+    """A line keeps its own frame and is sorted by its position along the axis (line_keys):
+    bit-exact against the oracle; the index's points are in axis order."""
+    p = {"random_line": _random_line, "axis_line": _axis_line}.get(gen, lambda n, s: GENERATORS["line"](n, seed=s))(
+        90_000, 7)
+    f = E.flat_frame(p.to(DEV))
+    assert isinstance(f, E.LineAxis)
+    idx = E.build_index(p.to(DEV), frame=f)
+    assert idx.qrot is None and idx.grid is None
+    t = (idx.pts[:idx.n] @ f.a).cpu()
+    assert bool((t[1:] >= t[:-1] - 1e-5).all())
+    _check(p, k, gen)
