@@ -582,8 +582,12 @@ def _refine_heavy_runs(points, skeys, perm):
     hs, hl = starts[heavy], lens[heavy]
     nh = int(hs.shape[0])
     m = int(hl.sum())
-    seg = torch.repeat_interleave(torch.arange(nh, device=dev, dtype=torch.int32), hl)  # [m]
     first = torch.cumsum(hl, 0) - hl                                          # run offsets in [m]
+    # run id of every position: a 1 at each run's first offset, prefix-summed (torch's
+    # repeat_interleave gives each run one thread: 3.9 ms for one 1e7-point run)
+    seg = torch.zeros(m, dtype=torch.int32, device=dev)
+    seg[first[1:]] = 1
+    seg = torch.cumsum(seg, 0, dtype=torch.int32)                              # [m]
     pos = hs[seg] + (torch.arange(m, device=dev) - first[seg])                # sorted positions
     del brk, starts, ends, lens, heavy
     src = perm[pos].long()

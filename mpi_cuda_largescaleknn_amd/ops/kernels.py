@@ -311,6 +311,7 @@ class FailWord:
         self._host = None
         self._ev = None
         self._gate = None
+        self.flist = None
 
     def stage(self, gate: torch.Tensor | None = None) -> None:
         """Queue the word's copy to pinned host memory on the current stream (right behind
@@ -492,7 +493,9 @@ def knn_gpu(qpts: torch.Tensor, nq: int, trees: list, k: int, cut2: float,
     a.wq = None
     # exact backstop over the failure list (device-side count: empty list = short no-op)
     check(lib.lsk_hip_knn_exact(C.byref(a), _ptr(flist), _ptr(count), cap, st), "knn_exact")
-    return FailWord(count, cap)
+    fw = FailWord(count, cap)
+    fw.flist = flist  # (debugging: the failed queries' positions, flist[:count])
+    return fw
 
 
 # --------------------------------------------------------------------------- cell grid
