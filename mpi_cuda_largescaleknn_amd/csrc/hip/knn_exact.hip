@@ -11,13 +11,14 @@
 // stackFree::knn (unorderedDataVariant.cu:84-86, 97-102), without its N*k heap memory.
 //
 // Per query (one wave, all control flow wave-uniform; a failure list gives each query a
-// block of 8 waves that split every tree's buckets and share the histogram):
+// block of 16 waves that split every tree's buckets and share the histogram; mixed-scale
+// 2e7 k=100 with 4 / 8 / 16 waves: 379 / 448 / 505 Mpts/s, profiles/r6_listwaves/):
 //  1. Upper bound: the max d² over k points taken around the query's position in
 //     tree 0 (queries are tree points in curve order, so these are spatial neighbours;
 //     any k distinct points give a valid bound), tightened by init_d2 when given, and
 //     clipped at the -r cutoff.
 //  2. Radix select on the float bits of d² in [lo, hi): every pass walks the bucket
-//     trees (DFS, 8-ary expansion tested by 8 lanes, stack in LDS), prunes boxes whose
+//     trees (DFS, 64-ary expansion tested by 64 lanes, stack in LDS), prunes boxes whose
 //     distance is >= hi and boxes whose farthest corner is closer than lo (their values
 //     were counted by an earlier pass: a thin shell through a dense far cluster visits
 //     only the buckets it cuts), counts a whole box at once when its [near, far] range
@@ -34,9 +35,23 @@ using lsk::bitsf;
 using lsk::fbits;
 
 constexpr int kWaves = 4;      // waves per block, one query each (whole-set runs)
-constexpr int kListWaves = 8;  // waves per block, all on one query (failure lists)
+#ifndef LSK_EXACT_LIST_WAVES
+#define LSK_EXACT_LIST_WAVES 16
+#endif
+constexpr int kListWaves = LSK_EXACT_LIST_WAVES;  // waves per block, all on one query (failure lists)
 constexpr int kBins = 256;
-constexpr int kStack = 128;  // DFS stack entries per wave (8-ary: <= 9 * 7 + 1 used)
+// levels per tree expansion: 3 = the 8 children of a node tested by 8 lanes, 6 = its 64
+// grandchildren by all 64 lanes (half the dependent node loads of a walk: the failure-list
+// walks are latency-bound; mixed-scale 2e7 k=100 at 16 waves 504 -> 512 Mpts/s)
+#ifndef LSK_EXACT_STEP
+#define LSK_EXACT_STEP 6
+#endif
+constexpr int kStep = LSK_EXACT_STEP;
+static_assert(kStep >= 1 && kStep <= 6, "a wave tests at most 64 boxes per expansion");
+// DFS stack entries per wave: <= ceil(30 / step) expansions of 2^step - 1 siblings + 1
+constexpr int kStack = ((30 + kStep - 1) / kStep * ((1 << kStep) - 1) + 1 + 31) / 32 * 32 < 128
+                           ? 128
+                           : ((30 + kStep - 1) / kStep * ((1 << kStep) - 1) + 1 + 31) / 32 * 32;
 
 // W = 1: each wave owns its query (hist per wave). W > 1: the block's W waves share one
 // query and one histogram, each walking a contiguous 1/W of every tree's buckets: the
@@ -100,7 +115,7 @@ __device__ void count_tree(const lsk_tree_view &T, float qx, float qy, float qz,
     }
     // expand to the descendants `step` levels down (at most the bucket level): lanes
     // 0..2^step-1 test one box each, the needed ones are pushed
-    const int32_t step = min(3, depth - lvl);
+    const int32_t step = min(kStep, depth - lvl);
     const uint32_t nc = 1u << step;
     const uint32_t child = (node << step) + (uint32_t)lane;
     bool need = false;
