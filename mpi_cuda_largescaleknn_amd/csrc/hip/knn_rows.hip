@@ -132,8 +132,14 @@ constexpr uint32_t kGuardRounds = 1u << 22;
 // step: queries next to a dense core far below their own scale (mixed_scale) would
 // otherwise stream millions of candidates through ONE wave, pass after pass, while the
 // rest of the GPU idles (2e7 points, k = 100: 0.26 s for the whole set).
-constexpr uint32_t kStepBudget = 8192;
-constexpr uint32_t kStepsPerK = 64;
+#ifndef LSK_STEP_BUDGET
+#define LSK_STEP_BUDGET 8192
+#endif
+#ifndef LSK_STEPS_PER_K
+#define LSK_STEPS_PER_K 64
+#endif
+constexpr uint32_t kStepBudget = LSK_STEP_BUDGET;
+constexpr uint32_t kStepsPerK = LSK_STEPS_PER_K;
 
 // LSK_PROFILE builds (tuning only) accumulate per-wave shader-clock cycles per activity
 // into stats[16..23]: proc hist, proc collect, traverse hist, traverse collect, replay

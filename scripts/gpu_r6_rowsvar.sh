@@ -2,7 +2,7 @@
 # knn_rows tuning constants on the sets it serves (clustered, planar, mixed-scale; 2e7,
 # k=100 / 16): library variants $VARIANTS (scripts/build_variant.py) vs production.
 source scripts/gpu_check.sh
-export TMPDIR=/tmp PYTHONUNBUFFERED=1 LSK_DISTS=clustered,planar,mixed_scale LSK_REPS=3
+export TMPDIR=/tmp PYTHONUNBUFFERED=1 LSK_DISTS=${LSK_DISTS:-clustered,planar,mixed_scale} LSK_REPS=3
 X=$PWD/mpi_cuda_largescaleknn_amd/lib/exp
 for v in base ${VARIANTS:-wpb1 wpb4} base; do
   if [ $v = base ]; then L=""; else L=$X/liblsknn_hip_$v.so; fi
